@@ -1,0 +1,209 @@
+/*
+ * gossip.h -- C ABI of the MI355X gossip-propagation engine (libgossip.so).
+ *
+ * Drop-in boundary for the reference's hot path
+ *     P2PNode::HandleRead -> seen-set check -> GossipShareToPeers
+ * (p2pnode.cc:127-199), which NS-3 drives one packet at a time through the socket
+ * receive callback bound at p2pnode.cc:74 and p2pnetwork.cc:142.  This ABI replaces
+ * that callback chain with a tick-synchronous bulk engine (one tick = --Latency) whose
+ * hot loop runs as hand-written gfx950 HIP kernels.
+ *
+ * Conventions
+ *   - Every call returns 0 on success or a negative GOSSIP_E* code; the text of the last
+ *     error on the calling thread is available from gossip_last_error().  No C++
+ *     exception crosses this boundary (the reference propagates no errors at all:
+ *     p2pnode.cc:147-151 silently erases a socket on a failed Send).
+ *   - Handles are opaque and NOT thread-safe per handle, like the single-threaded NS-3
+ *     event loop they replace (p2pnetwork.cc:216).
+ *   - Device buffers are engine-owned; host arrays are caller-owned and only read or
+ *     written during the call.
+ *   - There is no CPU fallback: without a HIP device gossip_engine_create fails.
+ */
+#ifndef GOSSIP_H
+#define GOSSIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GOSSIP_OK 0
+#define GOSSIP_EINVAL (-1)   /* bad argument                                  */
+#define GOSSIP_EHIP (-2)     /* HIP runtime error (no device, launch failure) */
+#define GOSSIP_ENOMEM (-3)   /* host or device allocation failed              */
+#define GOSSIP_ESTATE (-4)   /* call out of order (e.g. run before graph)     */
+#define GOSSIP_ECAPACITY (-5) /* live-share window exceeded the frontier capacity */
+
+const char* gossip_last_error(void);
+const char* gossip_version(void);
+
+/* ------------------------------------------------------------------------------------
+ * Time (ns-3 Time semantics, ns resolution).  Seconds()/MilliSeconds() as used at
+ * p2pnode.cc:101, p2pnetwork.cc:93,114,206: exact round-half-up of value*10^k.
+ * ---------------------------------------------------------------------------------- */
+int64_t gossip_seconds_to_ns(double seconds);
+int64_t gossip_milliseconds_to_ns(double ms);
+
+/* ------------------------------------------------------------------------------------
+ * Topology: replaces P2PGossipNetworkSimulation::CreateRandomTopology +
+ * ConnectNodes + makeconnections/ConnectPeerSockets + the REGISTER branch of HandleRead
+ * (p2pnetwork.cc:62-150, p2pnode.cc:77-89,178-188).
+ *
+ * A "link" is a key (a,b) of the reference's `connections` map (p2pnetwork.cc:30).
+ * Peer lists follow from the keys: key (a,b) puts b in peers(a) (AddPeer, de-duplicated)
+ * and a in peers(b) (REGISTER, not de-duplicated), so a parallel link gives multiplicity 2.
+ * ---------------------------------------------------------------------------------- */
+typedef struct gossip_topology gossip_topology;
+
+#define GOSSIP_TOPO_EXACT 0 /* the reference's mt19937 stream: O(n^2) draws, bit-exact   */
+#define GOSSIP_TOPO_SKIP 1  /* geometric skipping, Philox4x32-10 per row: O(links), for
+                               n far beyond the reference's limit; same fix-up rule      */
+
+int gossip_topology_create(uint32_t num_nodes, double connection_prob, uint32_t seed,
+                           int kind, int num_threads, gossip_topology** out);
+/* Import an explicit key list (e.g. a dump of an NS-3 run); keys are (a,b), a != b. */
+int gossip_topology_from_links(uint32_t num_nodes, uint64_t num_links, const uint32_t* a,
+                               const uint32_t* b, gossip_topology** out);
+uint32_t gossip_topology_num_nodes(const gossip_topology* t);
+uint64_t gossip_topology_num_links(const gossip_topology* t);
+/* Keys in std::map order. */
+int gossip_topology_get_links(const gossip_topology* t, uint32_t* a, uint32_t* b);
+/* Directed adjacency with multiplicity: CSR over distinct neighbours. */
+uint64_t gossip_topology_num_entries(const gossip_topology* t);
+int gossip_topology_get_csr(const gossip_topology* t, int64_t* row_ptr, int32_t* col,
+                            uint8_t* mult);
+/* Per node: |peers| (PrintStatistics "Peer count", p2pnetwork.cc:276) and
+ * |peersockets| ("Socket connections", :277). */
+int gossip_topology_get_degrees(const gossip_topology* t, uint32_t* peers, uint32_t* sockets);
+void gossip_topology_destroy(gossip_topology* t);
+
+/* ------------------------------------------------------------------------------------
+ * Share-generation schedule: replaces P2PNode's per-node mt19937 seeding and the
+ * ScheduleNextShare / GenerateAndGossipShare / GenerateUniqueShareId chain
+ * (p2pnode.cc:33-43, 91-125, 201-209).  Only COUNTED generations are emitted:
+ * t_start_ns <= t < t_cut_ns (earlier events hit the peers.empty() branch, later ones
+ * happen after PrintStatistics).
+ * ---------------------------------------------------------------------------------- */
+typedef struct gossip_gen_event {
+    int64_t ns;        /* Simulator::Now() at GenerateAndGossipShare        */
+    uint32_t node;     /* originNodeId                                      */
+    uint32_t share_id; /* GenerateUniqueShareId(): the seen-set key         */
+} gossip_gen_event;
+
+typedef struct gossip_schedule gossip_schedule;
+
+/* node_seed replaces std::random_device at p2pnode.cc:41 (node i seeds node_seed + i).
+ * id_mask != 0 ANDs every shareId (test knob that forces id collisions at small n).
+ * t_gen_end_ns (<= t_cut_ns, or 0 for t_cut_ns) stops emitting early for bounded runs. */
+int gossip_schedule_create(uint32_t num_nodes, uint32_t node_seed, int64_t t_start_ns,
+                           int64_t t_cut_ns, int64_t t_gen_end_ns, uint32_t id_mask,
+                           int num_threads, gossip_schedule** out);
+int gossip_schedule_from_events(uint64_t num_events, const gossip_gen_event* ev,
+                                gossip_schedule** out);
+uint64_t gossip_schedule_size(const gossip_schedule* s);
+/* Events sorted by (ns, node). */
+int gossip_schedule_get(const gossip_schedule* s, gossip_gen_event* out);
+void gossip_schedule_destroy(gossip_schedule* s);
+
+/* Multi-GPU sharding rule (the one every engine with shard_count > 1 applies): owner[k] =
+ * the shard that simulates event k.  Generations sharing an id inside one connected
+ * component (one seen-set entry, p2pnode.cc:189) always land on the same shard, so shards
+ * never interact and per-node counters add up exactly across shards. */
+int gossip_shard_events(const gossip_topology* t, uint64_t num_events, const gossip_gen_event* ev,
+                        uint32_t shard_count, uint32_t* owner);
+
+/* ------------------------------------------------------------------------------------
+ * Engine: replaces the per-packet HandleRead -> ReceiveShare -> GossipShareToPeers
+ * loop (p2pnode.cc:127-199) for all nodes at once, one tick (= Latency) per step.
+ * ---------------------------------------------------------------------------------- */
+typedef struct gossip_engine gossip_engine;
+
+#define GOSSIP_MODE_AUTO 0
+#define GOSSIP_MODE_CSR 1 /* bit-sliced frontier, CSR pull kernel              */
+
+typedef struct gossip_config {
+    uint32_t num_nodes;
+    int64_t latency_ns;   /* MilliSeconds(--Latency), channel Delay p2pnetwork.cc:114 */
+    int64_t t_start_ns;   /* makeconnections time, Seconds(5) p2pnetwork.cc:93        */
+    int64_t t_cut_ns;     /* PrintStatistics time, Seconds(simTime-0.1) :206           */
+    int32_t device;       /* HIP device ordinal                                        */
+    int32_t mode;         /* GOSSIP_MODE_*                                             */
+    uint32_t max_words;   /* frontier capacity, 64-share words per node (0 = auto)     */
+    uint32_t shard_rank;  /* share-class sharding across engines (multi-GPU)           */
+    uint32_t shard_count; /* 0 or 1 = no sharding                                      */
+    uint32_t flags;       /* GOSSIP_F_*                                                */
+} gossip_config;
+
+#define GOSSIP_F_TRACE 1u  /* record first-contact (node, shareId, tick) for tests  */
+#define GOSSIP_F_TIMING 2u /* time each pull-kernel launch with HIP events          */
+
+int gossip_engine_create(const gossip_config* cfg, gossip_engine** out);
+/* Graph: CSR over distinct neighbours with multiplicity in {1,2} (see topology above). */
+int gossip_engine_set_graph(gossip_engine* e, uint32_t num_nodes, const int64_t* row_ptr,
+                            const int32_t* col, const uint8_t* mult);
+int gossip_engine_set_topology(gossip_engine* e, const gossip_topology* t);
+/* Generation events (any order; the engine buckets them by tick). */
+int gossip_engine_set_schedule(gossip_engine* e, uint64_t num_events,
+                               const gossip_gen_event* ev);
+int gossip_engine_set_schedule_obj(gossip_engine* e, const gossip_schedule* s);
+/* Stats snapshots at absolute times (PrintPeriodicStats, p2pnetwork.cc:201-204). */
+int gossip_engine_add_snapshot(gossip_engine* e, int64_t t_ns);
+/* First tick of the run window (floor(t_start/L)) and one past the last tick. */
+int64_t gossip_engine_first_tick(const gossip_engine* e);
+int64_t gossip_engine_end_tick(const gossip_engine* e);
+int64_t gossip_engine_current_tick(const gossip_engine* e);
+/* Advance the simulation to tick_end (exclusive); returns when the work is enqueued
+ * and the host has caught up (call gossip_engine_sync to wait for the device). */
+int gossip_engine_run(gossip_engine* e, int64_t tick_end);
+int gossip_engine_sync(gossip_engine* e);
+
+/* Per-node report (PrintStatistics p2pnetwork.cc:271-277).  NULL pointers skipped. */
+int gossip_engine_get_stats(gossip_engine* e, uint32_t* gen, uint32_t* recv, uint32_t* fwd,
+                            uint64_t* sent, uint32_t* processed, uint32_t* peers,
+                            uint32_t* sockets);
+/* Snapshot k: time, total generated, total processed (uint64, no wrap). */
+int gossip_engine_get_snapshot(gossip_engine* e, uint32_t k, int64_t* t_ns,
+                               uint64_t* total_gen, uint64_t* total_processed);
+
+typedef struct gossip_counters {
+    uint64_t edge_events;      /* sum of sends so far (= "Total shares sent")      */
+    uint64_t receptions;       /* first arrivals (ReceiveShare calls)               */
+    uint64_t generations;      /* counted generations                               */
+    uint64_t ticks;            /* ticks simulated                                   */
+    uint64_t pull_launches;    /* pull-kernel launches                              */
+    double pull_ms;            /* summed HIP-event time of pull launches (TIMING)   */
+    uint64_t pull_bytes;       /* algorithmic bytes of those launches   */
+    uint32_t words_hw;         /* high-water frontier words per node                */
+    uint32_t words_cap;        /* frontier capacity (words per node)                */
+    uint64_t device_bytes;     /* device memory held by the engine                  */
+} gossip_counters;
+int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
+int gossip_engine_reset_timing(gossip_engine* e);
+
+/* First-contact trace (GOSSIP_F_TRACE): one record per (node, shareId) whose first
+ * contact happened in a simulated tick; via_recv=1 for ReceiveShare, 0 for own
+ * generation; hop = ticks since the winning source's generation. */
+uint64_t gossip_engine_trace_size(const gossip_engine* e);
+int gossip_engine_get_trace(const gossip_engine* e, uint32_t* node, uint32_t* share_id,
+                            int64_t* tick, uint32_t* hop, uint8_t* via_recv);
+
+void gossip_engine_destroy(gossip_engine* e);
+
+/* ------------------------------------------------------------------------------------
+ * Report: the exact NS_LOG_INFO lines of PrintStatistics (p2pnetwork.cc:255-284) and
+ * PrintPeriodicStats (:233-249), uint32 accumulators included.  Writes into buf
+ * (NUL-terminated) and returns the full length; call with buf=NULL to size it.
+ * ---------------------------------------------------------------------------------- */
+int64_t gossip_format_statistics(uint32_t num_nodes, const uint32_t* gen, const uint32_t* recv,
+                                 const uint32_t* fwd, const uint64_t* sent,
+                                 const uint32_t* processed, const uint32_t* peers,
+                                 const uint32_t* sockets, char* buf, uint64_t buf_len);
+int64_t gossip_format_periodic(double t_seconds, uint32_t num_nodes, uint64_t total_gen,
+                               uint64_t total_processed, uint64_t total_sockets, char* buf,
+                               uint64_t buf_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOSSIP_H */

@@ -1,0 +1,493 @@
+// oracle.cpp -- ORACLE A: event-driven CPU restatement of the reference's gossip path.
+//
+// TEST INFRASTRUCTURE ONLY (see oracle.h).  Nothing in the product links this file.
+//
+// What it restates, literally and single-threaded like the NS-3 simulator:
+//   * topology      CreateRandomTopology            p2pnetwork.cc:62-96  (+ConnectNodes :110-130)
+//   * peer lists    makeconnections/ConnectPeerSockets p2pnetwork.cc:99-107,133-150,
+//                   P2PNode::AddPeer p2pnode.cc:77-83, REGISTER branch p2pnode.cc:178-188
+//   * node RNG      P2PNode::P2PNode               p2pnode.cc:33-43  (rd() -> node_seed)
+//   * generation    ScheduleNextShare/GenerateAndGossipShare p2pnode.cc:97-125
+//   * share id      GenerateUniqueShareId           p2pnode.cc:201-209
+//   * hot path      GossipShareToPeers              p2pnode.cc:127-153
+//                   HandleRead (seen-set check)      p2pnode.cc:167-199
+//                   ReceiveShare                     p2pnode.cc:155-165
+//   * reporting     PrintStatistics                  p2pnetwork.cc:253-285
+//                   PrintPeriodicStats               p2pnetwork.cc:231-250
+//   * run window    Start                            p2pnetwork.cc:193-218
+//
+// The NS-3 transport is replaced by an ideal hop: a Send at time t is delivered (HandleRead)
+// at t + Latency.  Events at equal time run in scheduling order (NS-3's (ts, uid) order).
+// Time conversion follows ns-3's int64x64 path: Seconds(x) = round-half-up(x * 1e9) computed
+// exactly (not through a double product).  This is an assumption about the (unpinned) ns-3
+// version; see DESIGN.md.
+#include "oracle.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <memory>
+#include <queue>
+#include <random>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& m) {
+    g_err = m;
+    return -1;
+}
+
+// ns-3 int64x64: Seconds(double) -> From(int64x64_t(value), S) -> Time(v.Round()).
+// The double converts exactly into 64.64 fixed point; the product with 10^k is exact;
+// Round() is half away from zero.
+int64_t exact_scale_round(double x, uint64_t factor) {
+    if (x == 0.0) return 0;
+    const bool neg = x < 0;
+    double ax = neg ? -x : x;
+    int e2 = 0;
+    double m = std::frexp(ax, &e2);                          // ax = m * 2^e2, m in [0.5,1)
+    const uint64_t M = (uint64_t)std::ldexp(m, 53);           // exact 53-bit mantissa
+    const int sh = e2 - 53;                                    // ax = M * 2^sh
+    unsigned __int128 P = (unsigned __int128)M * factor;
+    unsigned __int128 q;
+    if (sh >= 0) {
+        q = P << sh;
+    } else {
+        const int s = -sh;
+        if (s >= 127) {
+            q = 0;
+        } else {
+            q = P >> s;
+            const unsigned __int128 rem = P - (q << s);
+            const unsigned __int128 half = (unsigned __int128)1 << (s - 1);
+            if (rem >= half) q += 1;
+        }
+    }
+    int64_t r = (int64_t)q;
+    return neg ? -r : r;
+}
+
+struct Share {
+    uint32_t origin;
+    uint32_t id;
+    int64_t ts;
+};
+
+struct Node {
+    uint32_t id = 0;
+    std::vector<uint32_t> peers;                  // p2pnode.h:32
+    std::unordered_set<uint32_t> peersockets;     // p2pnode.h:39 (keys only)
+    std::unordered_set<uint32_t> processed;       // p2pnode.h:38
+    std::mt19937 rng;                             // p2pnode.h:34
+    bool running = false;                         // p2pnode.h:36
+    uint32_t sent = 0, recv = 0, gen = 0, fwd = 0;  // p2pnode.h:40-43
+    uint64_t sent64 = 0;
+};
+
+enum EvType : uint32_t { EV_CONNECT, EV_GEN, EV_ARRIVE, EV_REGISTER, EV_PERIODIC, EV_STATS };
+
+struct Event {
+    int64_t t;
+    uint64_t seq;
+    uint32_t type;
+    uint32_t node;
+    uint32_t arg;  // share index (ARRIVE), peer id (REGISTER), replay-event index (GEN)
+    uint32_t hop;
+};
+struct EvLater {
+    bool operator()(const Event& a, const Event& b) const {
+        return a.t != b.t ? a.t > b.t : a.seq > b.seq;
+    }
+};
+
+struct TraceRec {
+    uint32_t node, id;
+    int64_t t;
+    uint32_t hop;
+    uint8_t via_recv;
+};
+
+}  // namespace
+
+struct oracle_sim {
+    bool replay = false;
+    uint32_t n = 0;
+    int64_t L = 0;            // hop delay (ns)
+    int64_t t_start = 0;      // makeconnections time (5 s)
+    int64_t t_cut = 0;        // PrintStatistics time (simTime - 0.1)
+    int64_t register_delay = 0;
+    uint32_t id_mask = 0;
+    std::vector<Node> nodes;
+    std::map<std::pair<uint32_t, uint32_t>, int> connections;  // p2pnetwork.cc:30
+    std::vector<Share> shares;
+    std::priority_queue<Event, std::vector<Event>, EvLater> q;
+    uint64_t seq = 0;
+    // replay inputs
+    std::vector<int64_t> rp_ns;
+    std::vector<uint32_t> rp_node, rp_id;
+    // outputs
+    std::vector<int64_t> gen_ns;
+    std::vector<uint32_t> gen_node, gen_id;
+    std::vector<int64_t> per_t;
+    std::vector<uint32_t> per_gen, per_proc, per_sock;
+    bool trace = false;
+    std::vector<TraceRec> tr;
+    // snapshot at PrintStatistics
+    bool have_stats = false;
+    std::vector<uint32_t> s_gen, s_recv, s_fwd, s_proc, s_peers, s_sock;
+    std::vector<uint64_t> s_sent;
+    uint64_t edge_events = 0, events = 0;
+    double wall = 0.0;
+
+    void schedule(int64_t t, uint32_t type, uint32_t node, uint32_t arg, uint32_t hop) {
+        q.push(Event{t, seq++, type, node, arg, hop});
+    }
+
+    // ConnectNodes (p2pnetwork.cc:110-130): only the map key matters here.
+    void connect_nodes(uint32_t i, uint32_t j) { connections[std::make_pair(i, j)] = 1; }
+
+    // P2PNode::AddPeer (p2pnode.cc:77-83): de-duplicated.
+    static void add_peer(Node& nd, uint32_t peer) {
+        if (std::find(nd.peers.begin(), nd.peers.end(), peer) == nd.peers.end())
+            nd.peers.push_back(peer);
+    }
+
+    // ScheduleNextShare (p2pnode.cc:97-104): U(2,5) s via libstdc++ generate_canonical.
+    void schedule_next_share(Node& nd, int64_t now) {
+        std::uniform_real_distribution<double> dist(2.0, 5.0);
+        const double next = dist(nd.rng);
+        schedule(now + exact_scale_round(next, 1000000000ull), EV_GEN, nd.id, 0, 0);
+    }
+
+    // GenerateUniqueShareId (p2pnode.cc:201-209); std::hash<uint64_t> is the identity.
+    uint32_t unique_share_id(const Node& nd, int64_t now) const {
+        const uint64_t seed = (uint64_t)nd.id * 1000000ull + (uint64_t)nd.gen * 1000ull +
+                              (uint64_t)(now % 1000);
+        uint32_t id = (uint32_t)std::hash<uint64_t>{}(seed);
+        if (id_mask) id &= id_mask;
+        return id;
+    }
+
+    // GossipShareToPeers (p2pnode.cc:127-153).  Send never fails at these loads.
+    void gossip(Node& nd, uint32_t share_idx, int64_t now, uint32_t hop) {
+        for (uint32_t peer : nd.peers) {
+            if (nd.peersockets.find(peer) == nd.peersockets.end()) continue;  // :131-135
+            nd.sent++;
+            nd.sent64++;
+            edge_events++;
+            schedule(now + L, EV_ARRIVE, peer, share_idx, hop + 1);
+        }
+    }
+
+    void record(uint32_t node, uint32_t id, int64_t t, uint32_t hop, uint8_t via) {
+        if (trace) tr.push_back(TraceRec{node, id, t, hop, via});
+    }
+
+    // GenerateAndGossipShare (p2pnode.cc:106-125).
+    void on_gen(const Event& e) {
+        Node& nd = nodes[e.node];
+        if (nd.peers.empty()) {                  // :108-113
+            if (!replay) schedule_next_share(nd, e.t);
+            return;
+        }
+        if (!nd.running) return;                 // :114
+        Share sh;
+        sh.origin = nd.id;
+        sh.id = replay ? rp_id[e.arg] : unique_share_id(nd, e.t);
+        nd.gen++;
+        sh.ts = e.t;
+        const bool was_seen = !nd.processed.insert(sh.id).second;
+        shares.push_back(sh);
+        gen_ns.push_back(e.t);
+        gen_node.push_back(nd.id);
+        gen_id.push_back(sh.id);
+        if (!was_seen) record(nd.id, sh.id, e.t, 0, 0);
+        gossip(nd, (uint32_t)(shares.size() - 1), e.t, 0);
+        if (!replay) schedule_next_share(nd, e.t);
+    }
+
+    // HandleRead (p2pnode.cc:167-199) for one SHARE message, then ReceiveShare (:155-165).
+    void on_arrive(const Event& e) {
+        Node& nd = nodes[e.node];
+        const Share& sh = shares[e.arg];
+        if (nd.processed.find(sh.id) != nd.processed.end()) return;  // :189-193 duplicate
+        nd.recv++;                                                   // ReceiveShare :157
+        nd.processed.insert(sh.id);                                  // :158
+        nd.fwd++;                                                    // :163
+        record(nd.id, sh.id, e.t, e.hop, 1);
+        gossip(nd, e.arg, e.t, e.hop);                               // :164
+    }
+
+    // makeconnections (p2pnetwork.cc:99-107) -> ConnectPeerSockets (:133-150).
+    void on_connect(const Event& e) {
+        for (const auto& kv : connections) {
+            const uint32_t i = kv.first.first, j = kv.first.second;
+            nodes[i].peersockets.insert(j);  // AddPeerSocket :144
+            add_peer(nodes[i], j);           // AddPeer :145
+            if (register_delay != 0) schedule(e.t + register_delay, EV_REGISTER, j, i, 0);
+        }
+        // "REGISTER:i" reaches node j in a later event (after every AddPeer of this loop has
+        // run); HandleRead :178-188 then appends i WITHOUT de-duplication.  The ideal model
+        // delivers them at t = 5 s, still after the whole makeconnections loop.
+        if (register_delay == 0)
+            for (const auto& kv : connections) {
+                const uint32_t i = kv.first.first, j = kv.first.second;
+                nodes[j].peersockets.insert(i);
+                nodes[j].peers.push_back(i);
+            }
+    }
+
+    void on_register(const Event& e) {
+        nodes[e.node].peersockets.insert(e.arg);
+        nodes[e.node].peers.push_back(e.arg);
+    }
+
+    // PrintPeriodicStats (p2pnetwork.cc:231-250): uint32 accumulators.
+    void on_periodic(const Event& e) {
+        uint32_t total_shares = 0, total_gen = 0, total_sock = 0;
+        for (const Node& nd : nodes) {
+            total_shares += (uint32_t)nd.processed.size();
+            total_gen += nd.gen;
+            total_sock += (uint32_t)nd.peersockets.size();
+        }
+        per_t.push_back(e.t);
+        per_gen.push_back(total_gen);
+        per_proc.push_back(total_shares);
+        per_sock.push_back(total_sock);
+    }
+
+    void on_stats() {
+        have_stats = true;
+        s_gen.resize(n); s_recv.resize(n); s_fwd.resize(n); s_proc.resize(n);
+        s_peers.resize(n); s_sock.resize(n); s_sent.resize(n);
+        for (uint32_t i = 0; i < n; i++) {
+            const Node& nd = nodes[i];
+            s_gen[i] = nd.gen; s_recv[i] = nd.recv; s_fwd[i] = nd.fwd;
+            s_sent[i] = nd.sent64; s_proc[i] = (uint32_t)nd.processed.size();
+            s_peers[i] = (uint32_t)nd.peers.size(); s_sock[i] = (uint32_t)nd.peersockets.size();
+        }
+    }
+};
+
+extern "C" {
+
+int64_t oracle_seconds_to_ns(double s) { return exact_scale_round(s, 1000000000ull); }
+int64_t oracle_milliseconds_to_ns(double ms) { return exact_scale_round(ms, 1000000ull); }
+
+const char* oracle_last_error(void) { return g_err.c_str(); }
+
+int oracle_create_reference(const oracle_params* p, oracle_sim** out) {
+    if (!p || !out) return fail("null argument");
+    if (p->num_nodes < 2)
+        return fail("numNodes < 2: the reference indexes nodes.Get(1) (p2pnetwork.cc:82)");
+    if (!(p->sim_time_s > 0.1)) return fail("simTime must exceed 0.1 s (p2pnetwork.cc:206)");
+    auto s = std::make_unique<oracle_sim>();
+    s->n = p->num_nodes;
+    s->L = exact_scale_round(p->latency_ms, 1000000ull);     // MilliSeconds(latencyMs) :114
+    s->t_start = exact_scale_round(5.0, 1000000000ull);      // Seconds(5) :93
+    s->t_cut = exact_scale_round(p->sim_time_s - 0.1, 1000000000ull);  // :206
+    s->register_delay = p->register_delay_ns;
+    s->id_mask = p->id_mask;
+    s->nodes.resize(s->n);
+    // P2PNode::P2PNode (p2pnode.cc:33-43): rng.seed(rd() + id).
+    for (uint32_t i = 0; i < s->n; i++) {
+        s->nodes[i].id = i;
+        s->nodes[i].rng.seed((uint32_t)(p->node_seed + i));
+    }
+    // CreateRandomTopology (p2pnetwork.cc:62-96).
+    {
+        std::mt19937 rng(p->topo_seed);
+        std::uniform_real_distribution<double> dist(0.0, 1.0);
+        const uint32_t n = s->n;
+        for (uint32_t i = 0; i < n; i++) {
+            bool connected = false;
+            for (uint32_t j = i + 1; j < n; j++) {
+                if (dist(rng) < p->connection_prob) {
+                    connected = true;
+                    s->connect_nodes(i, j);
+                }
+            }
+            if (!connected) {
+                if (i == 0) s->connect_nodes(0, 1);
+                else s->connect_nodes(i, i - 1);
+            }
+        }
+    }
+    // Event order mirrors the uids the reference hands out: makeconnections is scheduled
+    // in CreateRandomTopology (:93), then Start() schedules the first share of every node
+    // (:196-199), the periodic stats (:201-204), then PrintStatistics (:206).
+    s->schedule(s->t_start, EV_CONNECT, 0, 0, 0);
+    for (auto& nd : s->nodes) {
+        nd.running = true;                     // StartGeneratingShares p2pnode.cc:91-95
+        s->schedule_next_share(nd, 0);
+    }
+    for (double t = 10.0; t < p->sim_time_s; t += 10.0)
+        s->schedule(exact_scale_round(t, 1000000000ull), EV_PERIODIC, 0, 0, 0);
+    s->schedule(s->t_cut, EV_STATS, 0, 0, 0);
+    *out = s.release();
+    return 0;
+}
+
+int oracle_create_replay(uint32_t num_nodes, int64_t latency_ns, int64_t t_start_ns,
+                         int64_t t_cut_ns, uint64_t num_links, const uint32_t* link_a,
+                         const uint32_t* link_b, uint64_t num_events, const int64_t* ev_ns,
+                         const uint32_t* ev_node, const uint32_t* ev_id, oracle_sim** out) {
+    if (!out) return fail("null argument");
+    if (num_nodes < 1) return fail("num_nodes must be >= 1");
+    if (latency_ns <= 0) return fail("latency must be positive");
+    auto s = std::make_unique<oracle_sim>();
+    s->replay = true;
+    s->n = num_nodes;
+    s->L = latency_ns;
+    s->t_start = t_start_ns;
+    s->t_cut = t_cut_ns;
+    s->nodes.resize(num_nodes);
+    for (uint32_t i = 0; i < num_nodes; i++) {
+        s->nodes[i].id = i;
+        s->nodes[i].running = true;
+    }
+    for (uint64_t k = 0; k < num_links; k++) {
+        if (link_a[k] >= num_nodes || link_b[k] >= num_nodes) return fail("link out of range");
+        s->connect_nodes(link_a[k], link_b[k]);
+    }
+    s->rp_ns.assign(ev_ns, ev_ns + num_events);
+    s->rp_node.assign(ev_node, ev_node + num_events);
+    s->rp_id.assign(ev_id, ev_id + num_events);
+    s->schedule(s->t_start, EV_CONNECT, 0, 0, 0);
+    // Replay events carry the uids of generation events: earlier than any arrival.
+    std::vector<uint64_t> order(num_events);
+    for (uint64_t k = 0; k < num_events; k++) order[k] = k;
+    std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) {
+        return s->rp_ns[a] != s->rp_ns[b] ? s->rp_ns[a] < s->rp_ns[b]
+                                          : s->rp_node[a] < s->rp_node[b];
+    });
+    for (uint64_t k : order) {
+        if (s->rp_node[k] >= num_nodes) return fail("event node out of range");
+        if (s->rp_ns[k] < t_start_ns) return fail("replay event before t_start");
+        s->schedule(s->rp_ns[k], EV_GEN, s->rp_node[k], (uint32_t)k, 0);
+    }
+    if (t_cut_ns != std::numeric_limits<int64_t>::max())
+        s->schedule(t_cut_ns, EV_STATS, 0, 0, 0);
+    *out = s.release();
+    return 0;
+}
+
+int oracle_enable_trace(oracle_sim* s) {
+    if (!s) return fail("null sim");
+    s->trace = true;
+    return 0;
+}
+
+int oracle_run(oracle_sim* s) {
+    if (!s) return fail("null sim");
+    auto t0 = std::chrono::steady_clock::now();
+    while (!s->q.empty()) {
+        const Event e = s->q.top();
+        s->q.pop();
+        s->events++;
+        switch (e.type) {
+            case EV_CONNECT: s->on_connect(e); break;
+            case EV_GEN: s->on_gen(e); break;
+            case EV_ARRIVE: s->on_arrive(e); break;
+            case EV_REGISTER: s->on_register(e); break;
+            case EV_PERIODIC: s->on_periodic(e); break;
+            case EV_STATS: break;
+        }
+        if (e.type == EV_STATS) {
+            // StopAllNodes (same time, scheduled after PrintStatistics): nothing after
+            // this point is observable in the report.
+            s->on_stats();
+            break;
+        }
+    }
+    if (!s->have_stats) s->on_stats();
+    s->wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+int oracle_get_stats(const oracle_sim* s, uint32_t* gen, uint32_t* recv, uint32_t* fwd,
+                     uint64_t* sent, uint32_t* processed, uint32_t* peers, uint32_t* sockets) {
+    if (!s || !s->have_stats) return fail("no stats: run first");
+    const size_t n = s->n;
+    if (gen) std::memcpy(gen, s->s_gen.data(), n * 4);
+    if (recv) std::memcpy(recv, s->s_recv.data(), n * 4);
+    if (fwd) std::memcpy(fwd, s->s_fwd.data(), n * 4);
+    if (sent) std::memcpy(sent, s->s_sent.data(), n * 8);
+    if (processed) std::memcpy(processed, s->s_proc.data(), n * 4);
+    if (peers) std::memcpy(peers, s->s_peers.data(), n * 4);
+    if (sockets) std::memcpy(sockets, s->s_sock.data(), n * 4);
+    return 0;
+}
+
+int oracle_get_counters(const oracle_sim* s, uint64_t* edge_events, uint64_t* events,
+                        double* wall_s) {
+    if (!s) return fail("null sim");
+    if (edge_events) *edge_events = s->edge_events;
+    if (events) *events = s->events;
+    if (wall_s) *wall_s = s->wall;
+    return 0;
+}
+
+uint64_t oracle_get_links(const oracle_sim* s, uint32_t* a, uint32_t* b) {
+    if (!s) return 0;
+    uint64_t k = 0;
+    for (const auto& kv : s->connections) {
+        if (a) a[k] = kv.first.first;
+        if (b) b[k] = kv.first.second;
+        k++;
+    }
+    return k;
+}
+
+uint64_t oracle_get_gen_events(const oracle_sim* s, int64_t* ns, uint32_t* node, uint32_t* id) {
+    if (!s) return 0;
+    const uint64_t m = s->gen_ns.size();
+    for (uint64_t k = 0; k < m; k++) {
+        if (ns) ns[k] = s->gen_ns[k];
+        if (node) node[k] = s->gen_node[k];
+        if (id) id[k] = s->gen_id[k];
+    }
+    return m;
+}
+
+uint64_t oracle_get_periodic(const oracle_sim* s, int64_t* t_ns, uint32_t* total_gen,
+                             uint32_t* total_processed, uint32_t* total_sockets) {
+    if (!s) return 0;
+    const uint64_t m = s->per_t.size();
+    for (uint64_t k = 0; k < m; k++) {
+        if (t_ns) t_ns[k] = s->per_t[k];
+        if (total_gen) total_gen[k] = s->per_gen[k];
+        if (total_processed) total_processed[k] = s->per_proc[k];
+        if (total_sockets) total_sockets[k] = s->per_sock[k];
+    }
+    return m;
+}
+
+uint64_t oracle_get_trace(const oracle_sim* s, uint32_t* node, uint32_t* id, int64_t* t_ns,
+                          uint32_t* hop, uint8_t* via_recv) {
+    if (!s) return 0;
+    const uint64_t m = s->tr.size();
+    for (uint64_t k = 0; k < m; k++) {
+        const TraceRec& r = s->tr[k];
+        if (node) node[k] = r.node;
+        if (id) id[k] = r.id;
+        if (t_ns) t_ns[k] = r.t;
+        if (hop) hop[k] = r.hop;
+        if (via_recv) via_recv[k] = r.via_recv;
+    }
+    return m;
+}
+
+void oracle_destroy(oracle_sim* s) { delete s; }
+
+}  // extern "C"

@@ -1,0 +1,1158 @@
+// engine.hip -- MI355X (gfx950) tick-synchronous gossip engine behind the C ABI of gossip.h.
+//
+// Replaces the reference's per-packet hot path (P2PNode::HandleRead -> seen-set check ->
+// ReceiveShare -> GossipShareToPeers, p2pnode.cc:127-199) with one bulk step per tick
+// (tick = --Latency, the PointToPoint channel Delay of p2pnetwork.cc:114):
+//
+//   F_t[v]   = frontier: live share columns node v emitted (received or generated) in tick t
+//   inc[v]   = OR_{u in peers(v)} F_t[u]            (every emission reaches every peer, :129)
+//   new[v]   = inc[v] & ~seen[v]                      (processedShares check, :189)
+//   seen[v] |= new[v];  F_{t+1}[v] = new[v] | births  (ReceiveShare inserts + forwards, :155-165)
+//   recv[v] += popcount(new[v]); sent[v] += |peers(v)| * popcount(new[v])
+//
+// HBM layout (row-major, node rows): F0, F1, seen are n x stride uint64 words; bit b of word w
+// is share column 64w+b.  A column is one share source; shares whose 32-bit ids collide
+// (GenerateUniqueShareId, p2pnode.cc:201-209, collides above ~128,849 nodes) and that live in
+// one connected component form a "group": adjacent bits of one word, ordered by generation
+// phase, sharing one seen-set entry (the reference keys processedShares by id only).
+//
+// Kernels:
+//   k_pull   -- CSR pull over the bit-sliced frontier (HBM-bound: one neighbour row read per
+//               edge per tick, 16 B per lane, coalesced), seen/dedup, counters, liveness.
+//   k_births -- source injection (GenerateAndGossipShare, p2pnode.cc:106-125), including the
+//               same-tick "own generation vs arrival" rule for id groups.
+//   k_reduce -- counter reductions for snapshots / totals.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <numeric>
+#include <queue>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "internal.h"
+
+using gossip::set_error;
+
+namespace {
+
+#define HIP_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess)                                                          \
+            return set_error(GOSSIP_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+// Per-word control for one tick (host-built, uploaded each tick).
+struct WordCtl {
+    uint64_t clear;   // seen bits to clear before use (word re-allocated this tick)
+    uint64_t keep;    // columns that may receive this tick (phase cut at t_cut)
+    uint64_t gmask;   // bits that belong to multi-source id groups
+    uint64_t gstart;  // first bit of each group
+    uint64_t snap;    // columns whose arrivals count toward the snapshot partial
+};
+
+enum : uint32_t { BIRTH_NOOP = 0, BIRTH_NORMAL = 1, BIRTH_GROUP = 2 };
+
+struct Birth {
+    uint32_t node;
+    uint32_t col;    // word*64 + bit
+    int32_t phase;   // ns % L of the generation
+    uint32_t kind;   // BIRTH_*
+    uint32_t glo;    // group: first bit in word
+    uint32_t glen;   // group: number of bits
+    uint32_t poff;   // group: offset of member phases in the per-tick phase buffer
+    uint32_t pad;
+};
+
+struct PullArgs {
+    const int64_t* rowptr;
+    const int32_t* col;
+    const uint32_t* deg;
+    const uint64_t* Fcur;
+    uint64_t* Fnext;
+    uint64_t* seen;
+    const WordCtl* ctl;
+    uint32_t* recv;
+    uint64_t* sent;
+    unsigned long long* live;
+    unsigned long long* snap;  // nullable
+    uint32_t n;
+    uint32_t stride;
+    uint32_t wact;
+    uint32_t use_lds;
+};
+
+// Phase-ordered update of id groups inside one word (rare: only words holding groups).
+// Groups are contiguous bit ranges in phase order; a node's first contact with the id is
+// the lowest-phase arrival, and nothing arrives once any member bit is already seen.
+__device__ __forceinline__ uint64_t group_fix(uint64_t nw, uint64_t seen, uint64_t gm,
+                                              uint64_t gs) {
+    uint64_t rem = gm;
+    while (rem) {
+        const int s = __ffsll((long long)rem) - 1;
+        const uint64_t above = gs & ~((2ull << s) - 1ull);
+        const uint64_t upto = above ? ((above & (~above + 1ull)) - 1ull) : ~0ull;
+        const uint64_t grp = rem & upto;
+        if (seen & grp) {
+            nw &= ~grp;
+        } else {
+            const uint64_t x = nw & grp;
+            nw = (nw & ~grp) | (x & (~x + 1ull));
+        }
+        rem &= ~grp;
+    }
+    return nw;
+}
+
+// LPN = lanes per node (power of two).  Each lane owns two consecutive words (16 B) of a
+// 2*LPN-word pass; neighbour rows are read as 16-B vectors so a 64-lane group reads 1 KiB
+// of one row per instruction.  Several nodes share a wave when the live window is narrow.
+template <int LPN>
+__global__ __launch_bounds__(256) void k_pull(PullArgs a) {
+    constexpr int NPB = 256 / LPN;
+    extern __shared__ unsigned long long s_live[];
+    if (a.use_lds) {
+        for (uint32_t i = threadIdx.x; i < a.wact; i += 256) s_live[i] = 0ull;
+        __syncthreads();
+    }
+    const uint32_t sub = threadIdx.x % LPN;
+    const uint32_t slot = threadIdx.x / LPN;
+    const uint64_t stride = a.stride;
+    unsigned long long snap_local = 0ull;
+    for (uint64_t vb = (uint64_t)blockIdx.x * NPB; vb < a.n; vb += (uint64_t)gridDim.x * NPB) {
+        const uint64_t v = vb + slot;
+        if (v >= a.n) continue;  // uniform across the LPN lanes of a node
+        const int64_t beg = a.rowptr[v], end = a.rowptr[v + 1];
+        uint32_t cnt = 0;
+        for (uint32_t base = 0; base < a.wact; base += 2 * LPN) {
+            const uint32_t w = base + 2 * sub;
+            if (w >= a.wact) continue;
+            const uint64_t* Fw = a.Fcur + w;
+            uint64_t acc0 = 0ull, acc1 = 0ull;
+            int64_t j = beg;
+            for (; j + 4 <= end; j += 4) {
+                const uint64_t u0 = (uint32_t)a.col[j], u1 = (uint32_t)a.col[j + 1];
+                const uint64_t u2 = (uint32_t)a.col[j + 2], u3 = (uint32_t)a.col[j + 3];
+                const ulonglong2 q0 = *reinterpret_cast<const ulonglong2*>(Fw + u0 * stride);
+                const ulonglong2 q1 = *reinterpret_cast<const ulonglong2*>(Fw + u1 * stride);
+                const ulonglong2 q2 = *reinterpret_cast<const ulonglong2*>(Fw + u2 * stride);
+                const ulonglong2 q3 = *reinterpret_cast<const ulonglong2*>(Fw + u3 * stride);
+                acc0 |= (q0.x | q1.x) | (q2.x | q3.x);
+                acc1 |= (q0.y | q1.y) | (q2.y | q3.y);
+            }
+            for (; j < end; j++) {
+                const uint64_t u = (uint32_t)a.col[j];
+                const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(Fw + u * stride);
+                acc0 |= q.x;
+                acc1 |= q.y;
+            }
+            const WordCtl c0 = a.ctl[w], c1 = a.ctl[w + 1];
+            uint64_t* sp = a.seen + v * stride + w;
+            ulonglong2 s = *reinterpret_cast<const ulonglong2*>(sp);
+            s.x &= ~c0.clear;
+            s.y &= ~c1.clear;
+            uint64_t n0 = acc0 & ~s.x & c0.keep;
+            uint64_t n1 = acc1 & ~s.y & c1.keep;
+            if (c0.gmask) n0 = group_fix(n0, s.x, c0.gmask, c0.gstart);
+            if (c1.gmask) n1 = group_fix(n1, s.y, c1.gmask, c1.gstart);
+            if ((n0 | n1 | c0.clear | c1.clear) != 0ull) {
+                s.x |= n0;
+                s.y |= n1;
+                *reinterpret_cast<ulonglong2*>(sp) = s;
+            }
+            ulonglong2 o;
+            o.x = n0;
+            o.y = n1;
+            *reinterpret_cast<ulonglong2*>(a.Fnext + v * stride + w) = o;
+            cnt += (uint32_t)(__popcll(n0) + __popcll(n1));
+            if (a.snap) snap_local += (unsigned long long)(__popcll(n0 & c0.snap) + __popcll(n1 & c1.snap));
+            if (a.use_lds) {
+                if (n0) atomicOr(&s_live[w], (unsigned long long)n0);
+                if (n1) atomicOr(&s_live[w + 1], (unsigned long long)n1);
+            } else {
+                if (n0) atomicOr(&a.live[w], (unsigned long long)n0);
+                if (n1) atomicOr(&a.live[w + 1], (unsigned long long)n1);
+            }
+        }
+#pragma unroll
+        for (int off = LPN / 2; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, LPN);
+        if (sub == 0 && cnt) {
+            a.recv[v] += cnt;
+            a.sent[v] += (uint64_t)cnt * a.deg[v];
+        }
+    }
+    if (a.snap) {
+        for (int off = 32; off > 0; off >>= 1) snap_local += __shfl_xor(snap_local, off, 64);
+        if ((threadIdx.x & 63) == 0 && snap_local) atomicAdd(a.snap, snap_local);
+    }
+    if (a.use_lds) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
+            const unsigned long long x = s_live[i];
+            if (x) atomicOr(&a.live[i], x);
+        }
+    }
+}
+
+struct BirthArgs {
+    const Birth* b;
+    uint32_t nb;
+    const int32_t* gphase;
+    uint64_t* Fnext;
+    uint64_t* seen;
+    uint32_t stride;
+    uint32_t* gen;
+    uint32_t* recv;
+    uint32_t* effgen;
+    uint64_t* sent;
+    const uint32_t* deg;
+    unsigned long long* live;
+    unsigned long long* snap;  // nullable
+    int64_t snap_r;            // snapshot phase threshold (valid when snap != null)
+};
+
+// GenerateAndGossipShare (p2pnode.cc:106-125): gen++, insert, send to all peers -- sends and
+// the generation count happen even when the id is already in processedShares.  At most one
+// birth per node per tick (generation intervals are >= 2 s, latency < 2 s).
+__global__ __launch_bounds__(256) void k_births(BirthArgs a) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.nb) return;
+    const Birth x = a.b[i];
+    const uint64_t v = x.node;
+    const uint32_t dv = a.deg[v];
+    a.gen[v] += 1u;
+    a.sent[v] += dv;
+    if (x.kind == BIRTH_NOOP) return;
+    const uint32_t w = x.col >> 6;
+    const uint64_t bit = 1ull << (x.col & 63u);
+    uint64_t* fp = a.Fnext + v * a.stride + w;
+    uint64_t* sp = a.seen + v * a.stride + w;
+    bool eff = true;
+    if (x.kind == BIRTH_GROUP) {
+        const uint64_t gm = (x.glen >= 64 ? ~0ull : ((1ull << x.glen) - 1ull)) << x.glo;
+        const uint64_t arr = *fp & gm;
+        const uint64_t prior = (*sp & gm) & ~arr;
+        if (prior) {
+            eff = false;  // id already in processedShares before this tick
+        } else if (arr) {
+            const int ab = __ffsll((long long)arr) - 1;
+            const int32_t aph = a.gphase[x.poff + (uint32_t)ab - x.glo];
+            if (aph < x.phase) {
+                eff = false;  // the arrival came first in this tick
+            } else {
+                // Own generation first (ties: the generation event was scheduled earlier):
+                // the arrival finds the id already processed and is dropped.
+                *fp &= ~arr;
+                a.recv[v] -= 1u;
+                a.sent[v] -= dv;
+                if (a.snap && aph < a.snap_r) atomicAdd(a.snap, (unsigned long long)-1ll);
+            }
+        }
+    }
+    if (eff) {
+        *fp |= bit;
+        *sp |= bit;
+        a.effgen[v] += 1u;
+        atomicOr(&a.live[w], (unsigned long long)bit);
+        if (a.snap && x.phase < a.snap_r) atomicAdd(a.snap, 1ull);
+    }
+}
+
+// sum over nodes of (a[v] + b[v]) (b nullable) into *out (64-bit).
+__global__ __launch_bounds__(256) void k_sum_u32(const uint32_t* a, const uint32_t* b, uint32_t n,
+                                                 unsigned long long* out) {
+    unsigned long long s = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+        s += (unsigned long long)a[i] + (b ? b[i] : 0u);
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, s);
+}
+
+__global__ __launch_bounds__(256) void k_sum_u64(const uint64_t* a, uint32_t n,
+                                                 unsigned long long* out) {
+    unsigned long long s = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) s += a[i];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, s);
+}
+
+struct Instance {
+    uint32_t nsrc = 1;       // sources (share generations) in this instance
+    uint32_t first_ev = 0;   // index of rank-0 member in ev[] (groups: member list)
+    uint32_t word = 0;
+    uint8_t lo = 0;
+    uint8_t state = 0;       // 0 unallocated, 1 live, 2 retired
+};
+
+constexpr int kRing = 4;   // host staging slots
+constexpr int kLag = 2;    // ticks of lag before liveness is read back
+
+}  // namespace
+
+struct gossip_engine {
+    gossip_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool have_graph = false, have_sched = false;
+    // ---- graph
+    uint32_t n = 0;
+    uint64_t nnz = 0;
+    std::vector<int64_t> h_rowptr;
+    std::vector<int32_t> h_col;
+    std::vector<uint32_t> h_peers, h_sockets;
+    std::vector<uint32_t> comp;  // connected component label (computed on demand)
+    int64_t* d_rowptr = nullptr;
+    int32_t* d_col = nullptr;
+    uint32_t* d_deg = nullptr;
+    // ---- schedule (this shard)
+    std::vector<gossip_gen_event> ev;   // sorted by ns
+    std::vector<uint32_t> ev_inst;      // instance of each event
+    std::vector<uint8_t> ev_rank;       // bit rank inside its instance
+    std::vector<Instance> inst;
+    std::vector<uint32_t> grp_members;  // groups: event indices in rank order
+    std::vector<uint32_t> inst_moff;    // groups: offset in grp_members
+    std::vector<uint64_t> tick_lo;      // ev range per tick: [tick_lo[t-t0], tick_lo[t-t0+1])
+    uint32_t max_births = 0;
+    uint32_t max_group_phases = 0;
+    // ---- window / words
+    uint32_t stride = 0;     // words per node row (capacity, even)
+    uint32_t hw = 0;         // high-water words in use (even)
+    std::vector<WordCtl> ctl;
+    std::vector<int64_t> last_inject;
+    std::vector<uint8_t> word_alloc;
+    std::vector<std::vector<uint32_t>> word_insts;
+    std::vector<int32_t> col_phase;     // per column: generation phase (ns % L)
+    std::vector<uint32_t> col_src;      // per column: source event index
+    std::priority_queue<uint32_t, std::vector<uint32_t>, std::greater<uint32_t>> free_words;
+    int64_t open_word = -1;
+    uint32_t open_bit = 64;
+    std::vector<uint32_t> reset_now;    // words allocated this tick
+    // ---- time
+    int64_t L = 0, t0 = 0, tick0 = 0, tick_end = 0, cur = 0;
+    int64_t cut_tick = -1, cut_r = 0;
+    // ---- snapshots
+    struct Snap {
+        int64_t t_ns, tick, r;
+        uint64_t gen_total;
+    };
+    std::vector<Snap> snaps;
+    // ---- device state
+    uint64_t* d_F[2] = {nullptr, nullptr};
+    uint64_t* d_seen = nullptr;
+    uint32_t *d_recv = nullptr, *d_gen = nullptr, *d_effgen = nullptr;
+    uint64_t* d_sent = nullptr;
+    unsigned long long* d_live[2] = {nullptr, nullptr};
+    unsigned long long* d_scalars = nullptr;  // [0]=scratch, [1..]=snapshot base/partial
+    WordCtl* d_ctl[kRing] = {};
+    Birth* d_births[kRing] = {};
+    int32_t* d_gphase[kRing] = {};
+    int fcur = 0;
+    uint64_t device_bytes = 0;
+    // ---- host staging
+    WordCtl* h_ctl[kRing] = {};
+    Birth* h_births[kRing] = {};
+    int32_t* h_gphase[kRing] = {};
+    hipEvent_t slot_done[kRing] = {};
+    unsigned long long* h_live[kRing] = {};
+    hipEvent_t live_done[kRing] = {};
+    bool live_pending[kRing] = {};
+    int64_t live_tick[kRing] = {};
+    // ---- timing / counters
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timers;
+    std::vector<hipEvent_t> event_pool;
+    uint64_t pull_launches = 0, pull_bytes = 0, ticks = 0;
+    double pull_ms_done = 0.0;
+    // ---- trace
+    bool trace = false;
+    struct Tr {
+        uint32_t node, id;
+        int64_t tick;
+        uint32_t hop;
+        uint8_t via;
+    };
+    std::vector<Tr> tr;
+
+    ~gossip_engine();
+    int alloc_device();
+    int prepare_instances();
+    int compute_components();
+    int tick_step(int64_t t);
+    int retire_from(int64_t known_tick, const unsigned long long* live);
+    int alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t);
+    int decode_trace(int64_t t);
+    hipEvent_t get_event();
+};
+
+gossip_engine::~gossip_engine() {
+    if (stream) hipStreamSynchronize(stream);
+    for (auto& p : timers) {
+        hipEventDestroy(p.first);
+        hipEventDestroy(p.second);
+    }
+    for (auto e : event_pool) hipEventDestroy(e);
+    // Teardown: errors are ignored (nothing to report them to from a destructor).
+    hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
+    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen);
+    hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
+    hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_scalars);
+    for (int k = 0; k < kRing; k++) {
+        hipFree(d_ctl[k]); hipFree(d_births[k]); hipFree(d_gphase[k]);
+        hipHostFree(h_ctl[k]); hipHostFree(h_births[k]); hipHostFree(h_gphase[k]);
+        hipHostFree(h_live[k]);
+        if (slot_done[k]) hipEventDestroy(slot_done[k]);
+        if (live_done[k]) hipEventDestroy(live_done[k]);
+    }
+    if (stream) hipStreamDestroy(stream);
+}
+
+hipEvent_t gossip_engine::get_event() {
+    if (!event_pool.empty()) {
+        hipEvent_t e = event_pool.back();
+        event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    hipEventCreate(&e);
+    return e;
+}
+
+int gossip_engine::compute_components() {
+    if (comp.empty()) comp = gossip::components(n, h_rowptr.data(), h_col.data());
+    return GOSSIP_OK;
+}
+
+// Group generations into instances: (shareId, connected component).  Within a component a
+// later generation of an id either joins the live flood (a group) or finds the id already
+// processed everywhere (no-op); in different components the floods never meet.
+int gossip_engine::prepare_instances() {
+    const uint64_t m = ev.size();
+    const bool any_collision = gossip::any_id_collision(m, ev.data());
+    if (any_collision) compute_components();
+    // Key each event by (id, component); singles use their own index.
+    struct Key {
+        uint32_t id, comp, ev;
+    };
+    std::vector<Key> keys(m);
+    for (uint64_t k = 0; k < m; k++) {
+        const gossip_gen_event& e = ev[k];
+        keys[k] = Key{e.share_id, any_collision ? comp[e.node] : 0u, (uint32_t)k};
+    }
+    std::sort(keys.begin(), keys.end(), [&](const Key& a, const Key& b) {
+        if (a.id != b.id) return a.id < b.id;
+        if (a.comp != b.comp) return a.comp < b.comp;
+        const int64_t pa = ev[a.ev].ns % L, pb = ev[b.ev].ns % L;  // phase order
+        if (pa != pb) return pa < pb;
+        return ev[a.ev].ns != ev[b.ev].ns ? ev[a.ev].ns < ev[b.ev].ns : a.ev < b.ev;
+    });
+    // Shard ownership: deterministic hash of the instance key.
+    const uint32_t S = cfg.shard_count > 1 ? cfg.shard_count : 1;
+    std::vector<uint8_t> keep(m, 1);
+    std::vector<uint32_t> inst_of(m, 0);
+    std::vector<uint8_t> rank_of(m, 0);
+    inst.clear();
+    grp_members.clear();
+    inst_moff.clear();
+    uint64_t k = 0, id_end = 0;
+    while (k < m) {
+        uint64_t e = k + 1;
+        while (e < m && keys[e].id == keys[k].id && keys[e].comp == keys[k].comp) e++;
+        if (id_end <= k) {  // extent of this id over all components
+            id_end = e;
+            while (id_end < m && keys[id_end].id == keys[k].id) id_end++;
+        }
+        const bool lone = (id_end - k) == 1 && (e - k) == 1 && (k == 0 || keys[k - 1].id != keys[k].id);
+        const uint32_t ns = (uint32_t)(e - k);
+        if (ns > 64)
+            return set_error(GOSSIP_EINVAL, "more than 64 generations share one id in one component");
+        // Same rule as gossip_shard_events (host.cpp): lone ids by (id, node), others by
+        // (id, component).
+        const uint64_t hkey = lone ? gossip::instance_hash(keys[k].id, ev[keys[k].ev].node, true)
+                                   : gossip::instance_hash(keys[k].id, keys[k].comp, false);
+        const bool mine = S == 1 || (hkey % S) == cfg.shard_rank;
+        if (!mine) {
+            for (uint64_t q = k; q < e; q++) keep[keys[q].ev] = 0;
+        } else {
+            Instance I;
+            I.nsrc = ns;
+            I.first_ev = keys[k].ev;
+            const uint32_t id = (uint32_t)inst.size();
+            inst_moff.push_back((uint32_t)grp_members.size());
+            if (ns > 1)
+                for (uint64_t q = k; q < e; q++) grp_members.push_back(keys[q].ev);
+            for (uint64_t q = k; q < e; q++) {
+                inst_of[keys[q].ev] = id;
+                rank_of[keys[q].ev] = (uint8_t)(q - k);
+            }
+            inst.push_back(I);
+        }
+        k = e;
+    }
+    // Compact to the owned events (ev stays sorted by ns); remap member indices.
+    std::vector<uint32_t> newidx(m, UINT32_MAX);
+    std::vector<gossip_gen_event> ev2;
+    ev2.reserve(m);
+    ev_inst.clear();
+    ev_rank.clear();
+    for (uint64_t q = 0; q < m; q++) {
+        if (!keep[q]) continue;
+        newidx[q] = (uint32_t)ev2.size();
+        ev2.push_back(ev[q]);
+        ev_inst.push_back(inst_of[q]);
+        ev_rank.push_back(rank_of[q]);
+    }
+    for (auto& x : grp_members) x = newidx[x];
+    for (auto& I : inst) I.first_ev = newidx[I.first_ev];
+    ev.swap(ev2);
+    // Tick buckets.
+    const int64_t nt = tick_end - tick0 + 1;
+    tick_lo.assign((size_t)nt + 1, 0);
+    for (const auto& x : ev) {
+        const int64_t t = x.ns / L;
+        if (t < tick0 || t >= tick_end)
+            return set_error(GOSSIP_EINVAL, "generation event outside [t_start, t_cut)");
+        tick_lo[(size_t)(t - tick0) + 1]++;
+    }
+    max_births = 0;
+    for (int64_t t = 0; t < nt; t++) {
+        max_births = std::max<uint32_t>(max_births, (uint32_t)tick_lo[t + 1]);
+        tick_lo[t + 1] += tick_lo[t];
+    }
+    max_group_phases = 0;
+    for (int64_t t = 0; t < nt; t++) {
+        uint32_t s = 0;
+        for (uint64_t q = tick_lo[t]; q < tick_lo[t + 1]; q++) {
+            const Instance& I = inst[ev_inst[q]];
+            if (I.nsrc > 1) s += I.nsrc;
+        }
+        max_group_phases = std::max(max_group_phases, s);
+    }
+    return GOSSIP_OK;
+}
+
+int gossip_engine::alloc_device() {
+    // Capacity: peak births over a window of the estimated flood lifetime (BFS depth from a
+    // sample node + margin), unless the caller fixed max_words.
+    uint32_t words = cfg.max_words;
+    if (words == 0) {
+        // Flood lifetime estimate: the largest BFS depth from a few sample roots (host BFS
+        // over the CSR), plus the liveness read-back lag and slack.  Exceeding the estimate
+        // is reported as GOSSIP_ECAPACITY, never silently truncated.
+        int ecc = 0;
+        std::vector<int32_t> dist(n, -1);
+        std::vector<uint32_t> fr, nx;
+        const uint32_t roots[4] = {0u, n / 3u, (2u * n) / 3u, n - 1u};
+        for (uint32_t root : roots) {
+            std::fill(dist.begin(), dist.end(), -1);
+            fr.assign(1, root);
+            dist[root] = 0;
+            int depth = 0;
+            while (!fr.empty()) {
+                nx.clear();
+                for (uint32_t u : fr)
+                    for (int64_t j = h_rowptr[u]; j < h_rowptr[u + 1]; j++) {
+                        const uint32_t w = (uint32_t)h_col[j];
+                        if (dist[w] < 0) {
+                            dist[w] = dist[u] + 1;
+                            nx.push_back(w);
+                        }
+                    }
+                if (!nx.empty()) depth++;
+                fr.swap(nx);
+            }
+            ecc = std::max(ecc, depth);
+        }
+        const int64_t life = ecc + kLag + 4;
+        const int64_t nt = tick_end - tick0;
+        uint64_t peak = 0, run = 0;
+        std::vector<uint64_t> cnt((size_t)nt, 0);
+        for (int64_t t = 0; t < nt; t++) {
+            uint64_t c = 0;
+            for (uint64_t q = tick_lo[t]; q < tick_lo[t + 1]; q++) {
+                const Instance& I = inst[ev_inst[q]];
+                c += (ev_rank[q] == 0) ? I.nsrc : 0;
+            }
+            cnt[t] = c;
+            run += c;
+            if (t >= life) run -= cnt[t - life];
+            peak = std::max(peak, run);
+        }
+        uint64_t w = (peak + 63) / 64 + (uint64_t)life + 8;  // partial words per tick
+        w = (w + 1) & ~1ull;
+        words = (uint32_t)std::max<uint64_t>(w, 2);
+    }
+    stride = (words + 1) & ~1u;
+    const uint64_t bm = (uint64_t)n * stride * 8;
+    size_t freeb = 0, totalb = 0;
+    HIP_TRY(hipMemGetInfo(&freeb, &totalb));
+    const uint64_t need = 3 * bm + (uint64_t)n * 24 + (nnz * 4) + ((uint64_t)n + 1) * 8;
+    if (need > (uint64_t)freeb)
+        return set_error(GOSSIP_ENOMEM, "device memory: need " + std::to_string(need) +
+                                            " bytes for a " + std::to_string(stride) +
+                                            "-word window, " + std::to_string(freeb) + " free");
+    HIP_TRY(hipMalloc(&d_F[0], bm));
+    HIP_TRY(hipMalloc(&d_F[1], bm));
+    HIP_TRY(hipMalloc(&d_seen, bm));
+    HIP_TRY(hipMemsetAsync(d_F[0], 0, bm, stream));
+    HIP_TRY(hipMemsetAsync(d_F[1], 0, bm, stream));
+    HIP_TRY(hipMemsetAsync(d_seen, 0, bm, stream));
+    HIP_TRY(hipMalloc(&d_recv, (size_t)n * 4));
+    HIP_TRY(hipMalloc(&d_gen, (size_t)n * 4));
+    HIP_TRY(hipMalloc(&d_effgen, (size_t)n * 4));
+    HIP_TRY(hipMalloc(&d_sent, (size_t)n * 8));
+    HIP_TRY(hipMemsetAsync(d_recv, 0, (size_t)n * 4, stream));
+    HIP_TRY(hipMemsetAsync(d_gen, 0, (size_t)n * 4, stream));
+    HIP_TRY(hipMemsetAsync(d_effgen, 0, (size_t)n * 4, stream));
+    HIP_TRY(hipMemsetAsync(d_sent, 0, (size_t)n * 8, stream));
+    for (int k = 0; k < 2; k++) {
+        HIP_TRY(hipMalloc(&d_live[k], (size_t)stride * 8));
+        HIP_TRY(hipMemsetAsync(d_live[k], 0, (size_t)stride * 8, stream));
+    }
+    const size_t nsc = 2 + 2 * snaps.size();
+    HIP_TRY(hipMalloc(&d_scalars, nsc * 8));
+    HIP_TRY(hipMemsetAsync(d_scalars, 0, nsc * 8, stream));
+    const uint32_t bcap = std::max<uint32_t>(max_births, 1);
+    const uint32_t pcap = std::max<uint32_t>(max_group_phases, 1);
+    for (int k = 0; k < kRing; k++) {
+        HIP_TRY(hipMalloc(&d_ctl[k], (size_t)stride * sizeof(WordCtl)));
+        HIP_TRY(hipMalloc(&d_births[k], (size_t)bcap * sizeof(Birth)));
+        HIP_TRY(hipMalloc(&d_gphase[k], (size_t)pcap * 4));
+        HIP_TRY(hipHostMalloc(&h_ctl[k], (size_t)stride * sizeof(WordCtl), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&h_births[k], (size_t)bcap * sizeof(Birth), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&h_gphase[k], (size_t)pcap * 4, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&h_live[k], (size_t)stride * 8, hipHostMallocDefault));
+        HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&live_done[k], hipEventDisableTiming));
+    }
+    device_bytes = 3 * bm + (uint64_t)n * 20 + nnz * 4 + ((uint64_t)n + 1) * 8 + 2ull * stride * 8 +
+                   kRing * ((uint64_t)stride * sizeof(WordCtl) + (uint64_t)bcap * sizeof(Birth) + pcap * 4);
+    WordCtl z{0ull, ~0ull, 0ull, 0ull, 0ull};
+    ctl.assign(stride, z);
+    last_inject.assign(stride, INT64_MIN);
+    word_alloc.assign(stride, 0);
+    word_insts.assign(stride, {});
+    col_phase.assign((size_t)stride * 64, 0);
+    col_src.assign((size_t)stride * 64, UINT32_MAX);
+    HIP_TRY(hipStreamSynchronize(stream));
+    return GOSSIP_OK;
+}
+
+int gossip_engine::alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t) {
+    if (open_word < 0 || open_bit + k > 64) {
+        uint32_t w;
+        if (!free_words.empty()) {
+            w = free_words.top();
+            free_words.pop();
+        } else {
+            if (hw >= stride)
+                return set_error(GOSSIP_ECAPACITY,
+                                 "live-share window exceeded " + std::to_string(stride) +
+                                     " words per node; raise gossip_config.max_words");
+            w = hw++;
+            if (hw & 1u) {  // keep the processed width even (16-B vectors)
+                if (hw < stride) free_words.push(hw++);
+            }
+        }
+        word_alloc[w] = 1;
+        reset_now.push_back(w);
+        open_word = w;
+        open_bit = 0;
+    }
+    *word = (uint32_t)open_word;
+    *lo = (uint8_t)open_bit;
+    open_bit += k;
+    last_inject[*word] = t;
+    return GOSSIP_OK;
+}
+
+int gossip_engine::retire_from(int64_t known_tick, const unsigned long long* live) {
+    for (uint32_t w = 0; w < hw; w++) {
+        if (!word_alloc[w] || last_inject[w] > known_tick || live[w] != 0ull) continue;
+        for (uint32_t id : word_insts[w]) inst[id].state = 2;
+        word_insts[w].clear();
+        word_alloc[w] = 0;
+        ctl[w].gmask = 0ull;
+        ctl[w].gstart = 0ull;
+        for (int b = 0; b < 64; b++) col_src[(size_t)w * 64 + b] = UINT32_MAX;
+        free_words.push(w);
+        if ((int64_t)w == open_word) open_word = -1;
+    }
+    return GOSSIP_OK;
+}
+
+int gossip_engine::tick_step(int64_t t) {
+    const int slot = (int)(t % kRing);
+    // 1. liveness of tick t-kLag -> retire words whose floods have drained.
+    {
+        const int64_t kt = t - kLag;
+        const int ls = (int)(((kt % kRing) + kRing) % kRing);
+        if (kt >= tick0 && live_pending[ls] && live_tick[ls] == kt) {
+            HIP_TRY(hipEventSynchronize(live_done[ls]));
+            live_pending[ls] = false;
+            int rc = retire_from(kt, h_live[ls]);
+            if (rc) return rc;
+        }
+    }
+    // 2. staging slot reuse
+    HIP_TRY(hipEventSynchronize(slot_done[slot]));
+    // 3. births of tick t
+    reset_now.clear();
+    uint32_t nb = 0, np = 0;
+    const uint64_t lo = tick_lo[(size_t)(t - tick0)], hi = tick_lo[(size_t)(t - tick0) + 1];
+    Birth* B = h_births[slot];
+    int32_t* GP = h_gphase[slot];
+    for (uint64_t q = lo; q < hi; q++) {
+        const gossip_gen_event& e = ev[q];
+        Instance& I = inst[ev_inst[q]];
+        Birth b{};
+        b.node = e.node;
+        b.phase = (int32_t)(e.ns % L);
+        if (I.state == 2) {
+            b.kind = BIRTH_NOOP;
+        } else {
+            if (I.state == 0) {
+                uint32_t w;
+                uint8_t l;
+                int rc = alloc_bits(I.nsrc, &w, &l, t);
+                if (rc) return rc;
+                I.word = w;
+                I.lo = l;
+                I.state = 1;
+                word_insts[w].push_back(ev_inst[q]);
+                if (I.nsrc > 1) {
+                    const uint64_t gm = (I.nsrc >= 64 ? ~0ull : ((1ull << I.nsrc) - 1ull)) << l;
+                    ctl[w].gmask |= gm;
+                    ctl[w].gstart |= 1ull << l;
+                    const uint32_t off = inst_moff[ev_inst[q]];
+                    for (uint32_t r = 0; r < I.nsrc; r++) {
+                        const uint32_t m = grp_members[off + r];
+                        col_phase[(size_t)w * 64 + l + r] = (int32_t)(ev[m].ns % L);
+                        col_src[(size_t)w * 64 + l + r] = m;
+                    }
+                } else {
+                    col_phase[(size_t)w * 64 + l] = b.phase;
+                    col_src[(size_t)w * 64 + l] = (uint32_t)q;
+                }
+            }
+            last_inject[I.word] = t;
+            b.col = I.word * 64u + I.lo + ev_rank[q];
+            if (I.nsrc > 1) {
+                b.kind = BIRTH_GROUP;
+                b.glo = I.lo;
+                b.glen = I.nsrc;
+                b.poff = np;
+                for (uint32_t r = 0; r < I.nsrc; r++)
+                    GP[np++] = col_phase[(size_t)I.word * 64 + I.lo + r];
+            } else {
+                b.kind = BIRTH_NORMAL;
+            }
+        }
+        B[nb++] = b;
+    }
+    // 4. per-word control for this tick
+    for (uint32_t w : reset_now) ctl[w].clear = ~0ull;
+    const bool is_cut = (t == cut_tick && cut_r > 0);
+    int snap_idx = -1;
+    for (size_t s = 0; s < snaps.size(); s++)
+        if (snaps[s].tick == t && snaps[s].r > 0) snap_idx = (int)s;
+    WordCtl* C = h_ctl[slot];
+    for (uint32_t w = 0; w < hw; w++) {
+        WordCtl c = ctl[w];
+        if (is_cut || snap_idx >= 0) {
+            uint64_t km = 0ull, sm = 0ull;
+            for (int bb = 0; bb < 64; bb++) {
+                const int32_t ph = col_phase[(size_t)w * 64 + bb];
+                if (is_cut && ph < cut_r) km |= 1ull << bb;
+                if (snap_idx >= 0 && ph < snaps[snap_idx].r) sm |= 1ull << bb;
+            }
+            if (is_cut) c.keep = km;
+            if (snap_idx >= 0) c.snap = sm;
+        }
+        C[w] = c;
+    }
+    for (uint32_t w : reset_now) ctl[w].clear = 0ull;
+    // 5. upload + launches
+    const uint32_t wact = hw;
+    if (wact) HIP_TRY(hipMemcpyAsync(d_ctl[slot], C, (size_t)wact * sizeof(WordCtl), hipMemcpyHostToDevice, stream));
+    if (nb) HIP_TRY(hipMemcpyAsync(d_births[slot], B, (size_t)nb * sizeof(Birth), hipMemcpyHostToDevice, stream));
+    if (np) HIP_TRY(hipMemcpyAsync(d_gphase[slot], GP, (size_t)np * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipEventRecord(slot_done[slot], stream));
+    const int lv = (int)(t & 1);
+    if (wact) HIP_TRY(hipMemsetAsync(d_live[lv], 0, (size_t)wact * 8, stream));
+    unsigned long long* snap_ptr = snap_idx >= 0 ? d_scalars + 2 + 2 * snap_idx + 1 : nullptr;
+    const int nxt = fcur ^ 1;
+    if (wact) {
+        PullArgs a;
+        a.rowptr = d_rowptr; a.col = d_col; a.deg = d_deg;
+        a.Fcur = d_F[fcur]; a.Fnext = d_F[nxt]; a.seen = d_seen; a.ctl = d_ctl[slot];
+        a.recv = d_recv; a.sent = d_sent; a.live = d_live[lv]; a.snap = snap_ptr;
+        a.n = n; a.stride = stride; a.wact = wact;
+        a.use_lds = wact <= 8192 ? 1u : 0u;
+        int lpn = 1;
+        while (lpn < 64 && 2 * lpn < (int)wact) lpn *= 2;
+        const uint32_t npb = 256 / lpn;
+        const uint64_t groups = ((uint64_t)n + npb - 1) / npb;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(groups, 2048);
+        const size_t lds = a.use_lds ? (size_t)wact * 8 : 0;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (cfg.flags & GOSSIP_F_TIMING) {
+            e0 = get_event();
+            e1 = get_event();
+            HIP_TRY(hipEventRecord(e0, stream));
+        }
+        switch (lpn) {
+            case 1: k_pull<1><<<grid, 256, lds, stream>>>(a); break;
+            case 2: k_pull<2><<<grid, 256, lds, stream>>>(a); break;
+            case 4: k_pull<4><<<grid, 256, lds, stream>>>(a); break;
+            case 8: k_pull<8><<<grid, 256, lds, stream>>>(a); break;
+            case 16: k_pull<16><<<grid, 256, lds, stream>>>(a); break;
+            case 32: k_pull<32><<<grid, 256, lds, stream>>>(a); break;
+            default: k_pull<64><<<grid, 256, lds, stream>>>(a); break;
+        }
+        HIP_TRY(hipGetLastError());
+        if (cfg.flags & GOSSIP_F_TIMING) {
+            HIP_TRY(hipEventRecord(e1, stream));
+            timers.emplace_back(e0, e1);
+        }
+        pull_launches++;
+        pull_bytes += 8ull * (n + 1) + 4ull * nnz + 8ull * wact * nnz + 24ull * wact * n + 16ull * n;
+    }
+    if (nb) {
+        BirthArgs b;
+        b.b = d_births[slot]; b.nb = nb; b.gphase = d_gphase[slot];
+        b.Fnext = d_F[nxt]; b.seen = d_seen; b.stride = stride;
+        b.gen = d_gen; b.recv = d_recv; b.effgen = d_effgen; b.sent = d_sent; b.deg = d_deg;
+        b.live = d_live[lv]; b.snap = snap_ptr; b.snap_r = snap_idx >= 0 ? snaps[snap_idx].r : 0;
+        k_births<<<(nb + 255) / 256, 256, 0, stream>>>(b);
+        HIP_TRY(hipGetLastError());
+    }
+    // 6. liveness read-back (consumed kLag ticks later)
+    {
+        const int ls = (int)(t % kRing);
+        // Words at or beyond wact were allocated after this tick, so their last_inject is
+        // later than t and retire_from() never reads their (uncopied) entries.
+        if (wact) HIP_TRY(hipMemcpyAsync(h_live[ls], d_live[lv], (size_t)wact * 8, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipEventRecord(live_done[ls], stream));
+        live_pending[ls] = true;
+        live_tick[ls] = t;
+    }
+    // 7. snapshot bases: totals over ticks < snap.tick (the partial of snap.tick, if any,
+    //    is accumulated by that tick's pull/births through ctl.snap)
+    for (size_t s = 0; s < snaps.size(); s++) {
+        if (snaps[s].tick == t + 1) {
+            k_sum_u32<<<256, 256, 0, stream>>>(d_recv, d_effgen, n, d_scalars + 2 + 2 * s);
+            HIP_TRY(hipGetLastError());
+        }
+    }
+    fcur = nxt;
+    ticks++;
+    if (trace) {
+        int rc = decode_trace(t);
+        if (rc) return rc;
+    }
+    return GOSSIP_OK;
+}
+
+int gossip_engine::decode_trace(int64_t t) {
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (hw == 0) return GOSSIP_OK;
+    std::vector<uint64_t> F((size_t)n * stride);
+    HIP_TRY(hipMemcpy(F.data(), d_F[fcur], F.size() * 8, hipMemcpyDeviceToHost));
+    for (uint32_t v = 0; v < n; v++)
+        for (uint32_t w = 0; w < hw; w++) {
+            uint64_t x = F[(size_t)v * stride + w];
+            while (x) {
+                const int b = __builtin_ctzll(x);
+                x &= x - 1;
+                const uint32_t src = col_src[(size_t)w * 64 + b];
+                if (src == UINT32_MAX) continue;
+                const gossip_gen_event& e = ev[src];
+                const int64_t bt = e.ns / L;
+                const bool birth = (e.node == v && bt == t);
+                tr.push_back(Tr{v, e.share_id, t, (uint32_t)(t - bt), (uint8_t)(birth ? 0 : 1)});
+            }
+        }
+    return GOSSIP_OK;
+}
+
+extern "C" {
+
+int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
+    if (!cfg || !out) return set_error(GOSSIP_EINVAL, "NULL argument");
+    *out = nullptr;
+    if (cfg->latency_ns <= 0 || cfg->latency_ns >= 2000000000ll)
+        return set_error(GOSSIP_EINVAL,
+                         "latency must be in (0, 2 s): generation intervals are U(2,5) s "
+                         "(p2pnode.cc:99) and the engine allows one generation per node per tick");
+    if (cfg->t_cut_ns <= 0) return set_error(GOSSIP_EINVAL, "t_cut must be positive");
+    if (cfg->shard_count > 1 && cfg->shard_rank >= cfg->shard_count)
+        return set_error(GOSSIP_EINVAL, "shard_rank >= shard_count");
+    if (cfg->mode != GOSSIP_MODE_AUTO && cfg->mode != GOSSIP_MODE_CSR)
+        return set_error(GOSSIP_EINVAL, "unsupported mode");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return set_error(GOSSIP_EHIP, "no HIP device: the engine has no CPU fallback");
+    if (cfg->device < 0 || cfg->device >= ndev) return set_error(GOSSIP_EINVAL, "bad device ordinal");
+    try {
+        auto e = std::make_unique<gossip_engine>();
+        e->cfg = *cfg;
+        e->device = cfg->device;
+        HIP_TRY(hipSetDevice(e->device));
+        HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+        e->L = cfg->latency_ns;
+        e->t0 = cfg->t_start_ns;
+        e->tick0 = cfg->t_start_ns / e->L;
+        e->cut_tick = cfg->t_cut_ns / e->L;
+        e->cut_r = cfg->t_cut_ns % e->L;
+        e->tick_end = e->cut_r ? e->cut_tick + 1 : e->cut_tick;
+        if (e->tick_end < e->tick0) e->tick_end = e->tick0;
+        e->cur = e->tick0;
+        e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
+        *out = e.release();
+        return GOSSIP_OK;
+    } catch (const std::bad_alloc&) {
+        return set_error(GOSSIP_ENOMEM, "host allocation failed");
+    }
+}
+
+int gossip_engine_set_graph(gossip_engine* e, uint32_t num_nodes, const int64_t* row_ptr,
+                            const int32_t* col, const uint8_t* mult) {
+    if (!e || !row_ptr || (!col && row_ptr[num_nodes] > 0)) return set_error(GOSSIP_EINVAL, "NULL argument");
+    if (e->have_graph) return set_error(GOSSIP_ESTATE, "graph already set");
+    if (num_nodes != e->cfg.num_nodes) return set_error(GOSSIP_EINVAL, "num_nodes mismatch with config");
+    HIP_TRY(hipSetDevice(e->device));
+    try {
+        e->n = num_nodes;
+        e->nnz = (uint64_t)row_ptr[num_nodes];
+        if (e->nnz >= (1ull << 31)) return set_error(GOSSIP_EINVAL, "more than 2^31 adjacency entries");
+        e->h_rowptr.assign(row_ptr, row_ptr + num_nodes + 1);
+        e->h_col.assign(col, col + e->nnz);
+        e->h_peers.assign(num_nodes, 0);
+        e->h_sockets.assign(num_nodes, 0);
+        for (uint32_t v = 0; v < num_nodes; v++) {
+            if (row_ptr[v + 1] < row_ptr[v]) return set_error(GOSSIP_EINVAL, "row_ptr not monotone");
+            uint32_t p = 0;
+            for (int64_t j = row_ptr[v]; j < row_ptr[v + 1]; j++) {
+                if (col[j] < 0 || (uint32_t)col[j] >= num_nodes) return set_error(GOSSIP_EINVAL, "col out of range");
+                p += mult ? mult[j] : 1u;
+            }
+            e->h_peers[v] = p;
+            e->h_sockets[v] = (uint32_t)(row_ptr[v + 1] - row_ptr[v]);
+        }
+    } catch (const std::bad_alloc&) {
+        return set_error(GOSSIP_ENOMEM, "host allocation failed");
+    }
+    HIP_TRY(hipMalloc(&e->d_rowptr, ((size_t)e->n + 1) * 8));
+    HIP_TRY(hipMalloc(&e->d_col, std::max<size_t>(e->nnz, 1) * 4));
+    HIP_TRY(hipMalloc(&e->d_deg, (size_t)std::max<uint32_t>(e->n, 1) * 4));
+    HIP_TRY(hipMemcpy(e->d_rowptr, row_ptr, ((size_t)e->n + 1) * 8, hipMemcpyHostToDevice));
+    if (e->nnz) HIP_TRY(hipMemcpy(e->d_col, col, e->nnz * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->d_deg, e->h_peers.data(), (size_t)e->n * 4, hipMemcpyHostToDevice));
+    e->have_graph = true;
+    return GOSSIP_OK;
+}
+
+int gossip_engine_set_topology(gossip_engine* e, const gossip_topology* t) {
+    if (!t) return set_error(GOSSIP_EINVAL, "NULL topology");
+    return gossip_engine_set_graph(e, t->n, t->row_ptr.data(), t->col.data(), t->mult.data());
+}
+
+int gossip_engine_add_snapshot(gossip_engine* e, int64_t t_ns) {
+    if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    if (e->have_sched) return set_error(GOSSIP_ESTATE, "add snapshots before the schedule");
+    gossip_engine::Snap s{t_ns, t_ns / e->L, t_ns % e->L, 0};
+    for (const auto& o : e->snaps)
+        if (o.tick == s.tick) return set_error(GOSSIP_EINVAL, "two snapshots in one tick");
+    e->snaps.push_back(s);
+    return GOSSIP_OK;
+}
+
+int gossip_engine_set_schedule(gossip_engine* e, uint64_t num_events, const gossip_gen_event* ev) {
+    if (!e || (num_events && !ev)) return set_error(GOSSIP_EINVAL, "NULL argument");
+    if (!e->have_graph) return set_error(GOSSIP_ESTATE, "set the graph first");
+    if (e->have_sched) return set_error(GOSSIP_ESTATE, "schedule already set");
+    HIP_TRY(hipSetDevice(e->device));
+    try {
+        e->ev.assign(ev, ev + num_events);
+        for (const auto& x : e->ev) {
+            if (x.node >= e->n) return set_error(GOSSIP_EINVAL, "event node out of range");
+            if (x.ns < e->cfg.t_start_ns || x.ns >= e->cfg.t_cut_ns)
+                return set_error(GOSSIP_EINVAL, "event outside [t_start, t_cut): not a counted generation");
+        }
+        std::stable_sort(e->ev.begin(), e->ev.end(), [](const gossip_gen_event& a, const gossip_gen_event& b) {
+            return a.ns != b.ns ? a.ns < b.ns : a.node < b.node;
+        });
+        for (uint64_t k = 1; k < e->ev.size(); k++)
+            if (e->ev[k].node == e->ev[k - 1].node && e->ev[k].ns == e->ev[k - 1].ns)
+                return set_error(GOSSIP_EINVAL, "duplicate generation event");
+        int rc = e->prepare_instances();
+        if (rc) return rc;
+        for (auto& s : e->snaps) {
+            uint64_t g = 0;
+            for (const auto& x : e->ev)
+                if (x.ns < s.t_ns) g++;
+            s.gen_total = g;
+        }
+        rc = e->alloc_device();
+        if (rc) return rc;
+    } catch (const std::bad_alloc&) {
+        return set_error(GOSSIP_ENOMEM, "host allocation failed");
+    }
+    e->have_sched = true;
+    return GOSSIP_OK;
+}
+
+int gossip_engine_set_schedule_obj(gossip_engine* e, const gossip_schedule* s) {
+    if (!s) return set_error(GOSSIP_EINVAL, "NULL schedule");
+    return gossip_engine_set_schedule(e, s->ev.size(), s->ev.data());
+}
+
+int64_t gossip_engine_first_tick(const gossip_engine* e) { return e ? e->tick0 : -1; }
+int64_t gossip_engine_end_tick(const gossip_engine* e) { return e ? e->tick_end : -1; }
+int64_t gossip_engine_current_tick(const gossip_engine* e) { return e ? e->cur : -1; }
+
+int gossip_engine_run(gossip_engine* e, int64_t tick_end) {
+    if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    if (!e->have_sched) return set_error(GOSSIP_ESTATE, "set graph and schedule first");
+    HIP_TRY(hipSetDevice(e->device));
+    if (tick_end > e->tick_end) tick_end = e->tick_end;
+    try {
+        while (e->cur < tick_end) {
+            int rc = e->tick_step(e->cur);
+            if (rc) return rc;
+            e->cur++;
+        }
+    } catch (const std::bad_alloc&) {
+        return set_error(GOSSIP_ENOMEM, "host allocation failed");
+    }
+    return GOSSIP_OK;
+}
+
+int gossip_engine_sync(gossip_engine* e) {
+    if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return GOSSIP_OK;
+}
+
+int gossip_engine_get_stats(gossip_engine* e, uint32_t* gen, uint32_t* recv, uint32_t* fwd,
+                            uint64_t* sent, uint32_t* processed, uint32_t* peers,
+                            uint32_t* sockets) {
+    if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    if (!e->have_sched) return set_error(GOSSIP_ESTATE, "no schedule");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    const size_t n = e->n;
+    std::vector<uint32_t> r(n), g(n), eg(n);
+    HIP_TRY(hipMemcpy(r.data(), e->d_recv, n * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(g.data(), e->d_gen, n * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(eg.data(), e->d_effgen, n * 4, hipMemcpyDeviceToHost));
+    if (sent) HIP_TRY(hipMemcpy(sent, e->d_sent, n * 8, hipMemcpyDeviceToHost));
+    if (gen) std::memcpy(gen, g.data(), n * 4);
+    if (recv) std::memcpy(recv, r.data(), n * 4);
+    if (fwd) std::memcpy(fwd, r.data(), n * 4);  // sharesForwarded++ beside sharesReceived++
+    if (processed)
+        for (size_t i = 0; i < n; i++) processed[i] = r[i] + eg[i];
+    if (peers) std::memcpy(peers, e->h_peers.data(), n * 4);
+    if (sockets) std::memcpy(sockets, e->h_sockets.data(), n * 4);
+    return GOSSIP_OK;
+}
+
+int gossip_engine_get_snapshot(gossip_engine* e, uint32_t k, int64_t* t_ns, uint64_t* total_gen,
+                               uint64_t* total_processed) {
+    if (!e || k >= e->snaps.size()) return set_error(GOSSIP_EINVAL, "bad snapshot index");
+    if (!e->have_sched) return set_error(GOSSIP_ESTATE, "no schedule");
+    const auto& s = e->snaps[k];
+    if (e->cur <= s.tick - (s.r ? 0 : 1) && s.tick >= e->tick0)
+        return set_error(GOSSIP_ESTATE, "snapshot time not simulated yet");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    unsigned long long v[2] = {0, 0};
+    HIP_TRY(hipMemcpy(v, e->d_scalars + 2 + 2 * k, 16, hipMemcpyDeviceToHost));
+    if (t_ns) *t_ns = s.t_ns;
+    if (total_gen) *total_gen = s.gen_total;
+    if (total_processed) *total_processed = (s.tick <= e->tick0 && s.r == 0) ? 0 : (v[0] + v[1]);
+    return GOSSIP_OK;
+}
+
+int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
+    if (!e || !c) return set_error(GOSSIP_EINVAL, "NULL argument");
+    std::memset(c, 0, sizeof(*c));
+    c->ticks = e->ticks;
+    c->pull_launches = e->pull_launches;
+    c->pull_bytes = e->pull_bytes;
+    c->words_hw = e->hw;
+    c->words_cap = e->stride;
+    c->device_bytes = e->device_bytes;
+    if (!e->have_sched) return GOSSIP_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    double ms = e->pull_ms_done;
+    for (auto& p : e->timers) {
+        float x = 0.f;
+        HIP_TRY(hipEventElapsedTime(&x, p.first, p.second));
+        ms += x;
+        e->event_pool.push_back(p.first);
+        e->event_pool.push_back(p.second);
+    }
+    e->timers.clear();
+    e->pull_ms_done = ms;
+    c->pull_ms = ms;
+    HIP_TRY(hipMemsetAsync(e->d_scalars, 0, 16, e->stream));
+    k_sum_u64<<<256, 256, 0, e->stream>>>(e->d_sent, e->n, e->d_scalars);
+    k_sum_u32<<<256, 256, 0, e->stream>>>(e->d_recv, nullptr, e->n, e->d_scalars + 1);
+    HIP_TRY(hipGetLastError());
+    unsigned long long v[2];
+    HIP_TRY(hipMemcpyAsync(v, e->d_scalars, 16, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    c->edge_events = v[0];
+    c->receptions = v[1];
+    uint64_t g = 0;
+    const uint64_t done = (uint64_t)std::max<int64_t>(0, std::min(e->cur, e->tick_end) - e->tick0);
+    if (!e->tick_lo.empty()) g = e->tick_lo[std::min<uint64_t>(done, e->tick_lo.size() - 1)];
+    c->generations = g;
+    return GOSSIP_OK;
+}
+
+int gossip_engine_reset_timing(gossip_engine* e) {
+    if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (auto& p : e->timers) {
+        e->event_pool.push_back(p.first);
+        e->event_pool.push_back(p.second);
+    }
+    e->timers.clear();
+    e->pull_ms_done = 0.0;
+    e->pull_launches = 0;
+    e->pull_bytes = 0;
+    return GOSSIP_OK;
+}
+
+uint64_t gossip_engine_trace_size(const gossip_engine* e) { return e ? e->tr.size() : 0; }
+
+int gossip_engine_get_trace(const gossip_engine* e, uint32_t* node, uint32_t* share_id,
+                            int64_t* tick, uint32_t* hop, uint8_t* via_recv) {
+    if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    for (size_t k = 0; k < e->tr.size(); k++) {
+        const auto& r = e->tr[k];
+        if (node) node[k] = r.node;
+        if (share_id) share_id[k] = r.id;
+        if (tick) tick[k] = r.tick;
+        if (hop) hop[k] = r.hop;
+        if (via_recv) via_recv[k] = r.via;
+    }
+    return GOSSIP_OK;
+}
+
+void gossip_engine_destroy(gossip_engine* e) {
+    if (!e) return;
+    hipSetDevice(e->device);
+    delete e;
+}
+
+}  // extern "C"

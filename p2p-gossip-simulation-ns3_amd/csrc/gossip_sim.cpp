@@ -1,0 +1,262 @@
+// gossip_sim.cpp -- command-line driver: the drop-in replacement for the reference's main()
+// (p2pnetwork.cc:289-313) and P2PGossipNetworkSimulation (p2pnetwork.cc:15-286), with the
+// NS-3 event loop replaced by the MI355X engine of libgossip.so.
+//
+//   gossip_sim --numNodes=10 --connectionProb=0.3 --simTime=60 --Latency=5
+//
+// Same four flags and defaults as the reference (p2pnetwork.cc:294-306, ns3::CommandLine
+// syntax --name=value; "--name value" is accepted too).  std::random_device is replaced by
+// explicit seeds (--seed for the topology, --nodeSeed for the per-node share RNGs), printed
+// so that a run can be reproduced.  The report is the reference's NS_LOG_INFO text.
+#include <cerrno>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gossip.h"
+
+namespace {
+
+struct Options {
+    uint32_t numNodes = 10;            // p2pnetwork.cc:294
+    double connectionProb = 0.3;       // :295
+    double simTime = 60.0;             // :296
+    double latencyMs = 5.0;            // :297
+    uint32_t seed = 1;                 // replaces rd() at p2pnetwork.cc:65
+    uint32_t nodeSeed = 1000;          // replaces rd() at p2pnode.cc:41
+    std::string topology = "auto";     // exact | skip | auto
+    int device = 0;
+    int threads = 8;
+    uint32_t maxWords = 0;
+    bool quiet = false;                // totals only (no per-node lines)
+    bool periodic = true;
+    bool timing = false;
+    std::string dumpLinks, dumpEvents, linksIn, eventsIn;
+};
+
+void usage() {
+    std::fprintf(stderr,
+                 "usage: gossip_sim [--numNodes=N] [--connectionProb=P] [--simTime=S] "
+                 "[--Latency=MS]\n"
+                 "                  [--seed=S] [--nodeSeed=S] [--topology=auto|exact|skip]\n"
+                 "                  [--device=D] [--threads=T] [--maxWords=W] [--quiet]\n"
+                 "                  [--noPeriodic] [--timing] [--dumpLinks=F] [--dumpEvents=F]\n"
+                 "                  [--links=F] [--events=F]\n");
+}
+
+bool parse(int argc, char** argv, Options& o) {
+    for (int i = 1; i < argc; i++) {
+        std::string a = argv[i];
+        if (a == "--help" || a == "-h") return false;
+        if (a.rfind("--", 0) != 0) {
+            std::fprintf(stderr, "unexpected argument '%s'\n", a.c_str());
+            return false;
+        }
+        std::string key = a.substr(2), val;
+        const size_t eq = key.find('=');
+        bool has_val = eq != std::string::npos;
+        if (has_val) {
+            val = key.substr(eq + 1);
+            key = key.substr(0, eq);
+        }
+        auto need = [&]() -> bool {
+            if (has_val) return true;
+            if (i + 1 < argc) {
+                val = argv[++i];
+                return true;
+            }
+            std::fprintf(stderr, "missing value for --%s\n", key.c_str());
+            return false;
+        };
+        auto num = [&](double& d) -> bool {
+            if (!need()) return false;
+            char* end = nullptr;
+            errno = 0;
+            d = std::strtod(val.c_str(), &end);
+            if (errno || end == val.c_str() || *end) {
+                std::fprintf(stderr, "invalid value '%s' for --%s\n", val.c_str(), key.c_str());
+                return false;
+            }
+            return true;
+        };
+        double d = 0;
+        if (key == "numNodes") { if (!num(d) || d < 0 || d > 4294967295.0) return false; o.numNodes = (uint32_t)d; }
+        else if (key == "connectionProb") { if (!num(o.connectionProb)) return false; }
+        else if (key == "simTime") { if (!num(o.simTime)) return false; }
+        else if (key == "Latency") { if (!num(o.latencyMs)) return false; }
+        else if (key == "seed") { if (!num(d)) return false; o.seed = (uint32_t)d; }
+        else if (key == "nodeSeed") { if (!num(d)) return false; o.nodeSeed = (uint32_t)d; }
+        else if (key == "device") { if (!num(d)) return false; o.device = (int)d; }
+        else if (key == "threads") { if (!num(d)) return false; o.threads = (int)d; }
+        else if (key == "maxWords") { if (!num(d)) return false; o.maxWords = (uint32_t)d; }
+        else if (key == "topology") { if (!need()) return false; o.topology = val; }
+        else if (key == "quiet") o.quiet = true;
+        else if (key == "noPeriodic") o.periodic = false;
+        else if (key == "timing") o.timing = true;
+        else if (key == "dumpLinks") { if (!need()) return false; o.dumpLinks = val; }
+        else if (key == "dumpEvents") { if (!need()) return false; o.dumpEvents = val; }
+        else if (key == "links") { if (!need()) return false; o.linksIn = val; }
+        else if (key == "events") { if (!need()) return false; o.eventsIn = val; }
+        else {
+            std::fprintf(stderr, "unknown option --%s\n", key.c_str());
+            return false;
+        }
+    }
+    return true;
+}
+
+int die(const char* what) {
+    std::fprintf(stderr, "gossip_sim: %s failed: %s\n", what, gossip_last_error());
+    return 1;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    Options o;
+    if (!parse(argc, argv, o)) {
+        usage();
+        return 2;
+    }
+    const int64_t L = gossip_milliseconds_to_ns(o.latencyMs);          // p2pnetwork.cc:114
+    const int64_t t_start = gossip_seconds_to_ns(5.0);                 // :93
+    const int64_t t_cut = gossip_seconds_to_ns(o.simTime - 0.1);       // :206
+    if (!(o.simTime > 0.1)) {
+        std::fprintf(stderr, "gossip_sim: --simTime must exceed 0.1 s\n");
+        return 2;
+    }
+
+    // ---- CreateRandomTopology (p2pnetwork.cc:62-96) ----
+    gossip_topology* topo = nullptr;
+    if (!o.linksIn.empty()) {
+        FILE* f = std::fopen(o.linksIn.c_str(), "r");
+        if (!f) { std::perror(o.linksIn.c_str()); return 1; }
+        std::vector<uint32_t> a, b;
+        unsigned x, y;
+        while (std::fscanf(f, "%u %u", &x, &y) == 2) { a.push_back(x); b.push_back(y); }
+        std::fclose(f);
+        if (gossip_topology_from_links(o.numNodes, a.size(), a.data(), b.data(), &topo)) return die("topology import");
+    } else {
+        int kind = GOSSIP_TOPO_EXACT;
+        if (o.topology == "skip" || (o.topology == "auto" && o.numNodes > 16384)) kind = GOSSIP_TOPO_SKIP;
+        else if (o.topology != "exact" && o.topology != "auto") { usage(); return 2; }
+        if (gossip_topology_create(o.numNodes, o.connectionProb, o.seed, kind, o.threads, &topo))
+            return die("topology");
+    }
+    const uint32_t n = gossip_topology_num_nodes(topo);
+
+    // ---- share schedule (P2PNode RNGs, p2pnode.cc:33-43, 91-125) ----
+    gossip_schedule* sched = nullptr;
+    if (!o.eventsIn.empty()) {
+        FILE* f = std::fopen(o.eventsIn.c_str(), "r");
+        if (!f) { std::perror(o.eventsIn.c_str()); return 1; }
+        std::vector<gossip_gen_event> ev;
+        long long ns;
+        unsigned node, id;
+        while (std::fscanf(f, "%lld %u %u", &ns, &node, &id) == 3) ev.push_back({ns, node, id});
+        std::fclose(f);
+        if (gossip_schedule_from_events(ev.size(), ev.data(), &sched)) return die("schedule import");
+    } else if (gossip_schedule_create(n, o.nodeSeed, t_start, t_cut, 0, 0, o.threads, &sched)) {
+        return die("schedule");
+    }
+    if (!o.dumpLinks.empty()) {
+        std::vector<uint32_t> a(gossip_topology_num_links(topo)), b(a.size());
+        gossip_topology_get_links(topo, a.data(), b.data());
+        FILE* f = std::fopen(o.dumpLinks.c_str(), "w");
+        for (size_t k = 0; f && k < a.size(); k++) std::fprintf(f, "%u %u\n", a[k], b[k]);
+        if (f) std::fclose(f);
+    }
+    if (!o.dumpEvents.empty()) {
+        std::vector<gossip_gen_event> ev(gossip_schedule_size(sched));
+        gossip_schedule_get(sched, ev.data());
+        FILE* f = std::fopen(o.dumpEvents.c_str(), "w");
+        for (size_t k = 0; f && k < ev.size(); k++)
+            std::fprintf(f, "%lld %u %u\n", (long long)ev[k].ns, ev[k].node, ev[k].share_id);
+        if (f) std::fclose(f);
+    }
+
+    // ---- engine ----
+    gossip_config cfg{};
+    cfg.num_nodes = n;
+    cfg.latency_ns = L;
+    cfg.t_start_ns = t_start;
+    cfg.t_cut_ns = t_cut;
+    cfg.device = o.device;
+    cfg.mode = GOSSIP_MODE_AUTO;
+    cfg.max_words = o.maxWords;
+    cfg.flags = o.timing ? GOSSIP_F_TIMING : 0u;
+    gossip_engine* eng = nullptr;
+    if (gossip_engine_create(&cfg, &eng)) return die("engine create");
+    if (gossip_engine_set_topology(eng, topo)) return die("engine graph");
+    std::vector<double> per_t;
+    if (o.periodic)
+        for (double t = 10.0; t < o.simTime; t += 10.0) {  // Start(): p2pnetwork.cc:201-204
+            if (gossip_engine_add_snapshot(eng, gossip_seconds_to_ns(t))) return die("snapshot");
+            per_t.push_back(t);
+        }
+    if (gossip_engine_set_schedule_obj(eng, sched)) return die("engine schedule");
+
+    std::printf("Starting gossip network simulation for %g seconds\n", o.simTime);
+    std::printf("seeds: topology %u, nodes %u; latency %lld ns; ticks [%lld, %lld)\n", o.seed,
+                o.nodeSeed, (long long)L, (long long)gossip_engine_first_tick(eng),
+                (long long)gossip_engine_end_tick(eng));
+    auto w0 = std::chrono::steady_clock::now();
+    if (gossip_engine_run(eng, gossip_engine_end_tick(eng))) return die("engine run");
+    if (gossip_engine_sync(eng)) return die("engine sync");
+    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
+
+    std::vector<uint32_t> gen(n), recv(n), fwd(n), proc(n), peers(n), sock(n);
+    std::vector<uint64_t> sent(n);
+    if (gossip_engine_get_stats(eng, gen.data(), recv.data(), fwd.data(), sent.data(), proc.data(),
+                                peers.data(), sock.data()))
+        return die("stats");
+    uint64_t total_sock = 0;
+    for (uint32_t v = 0; v < n; v++) total_sock += sock[v];
+    for (size_t k = 0; k < per_t.size(); k++) {
+        int64_t tns;
+        uint64_t tg, tp;
+        if (gossip_engine_get_snapshot(eng, (uint32_t)k, &tns, &tg, &tp)) return die("snapshot read");
+        const uint64_t sockets_now = tns >= t_start ? total_sock : 0;
+        std::string buf((size_t)gossip_format_periodic(per_t[k], n, tg, tp, sockets_now, nullptr, 0) + 1, '\0');
+        gossip_format_periodic(per_t[k], n, tg, tp, sockets_now, &buf[0], buf.size());
+        std::fputs(buf.c_str(), stdout);
+    }
+    if (t_cut < t_start)  // PrintStatistics before makeconnections: no peers, no sockets yet
+        for (uint32_t v = 0; v < n; v++) peers[v] = sock[v] = 0;
+    if (o.quiet) {
+        uint32_t tg = 0, tr = 0, tf = 0, ts = 0, tc = 0;
+        for (uint32_t v = 0; v < n; v++) {
+            tg += gen[v]; tr += recv[v]; tf += fwd[v]; ts += (uint32_t)sent[v]; tc += sock[v];
+        }
+        std::printf("=== P2P Gossip Network Simulation Statistics ===\n");
+        std::printf("Total shares generated: %u\nTotal shares received: %u\nTotal shares forwarded: %u\n"
+                    "Total shares sent: %u\nTotal socket connections: %u\n", tg, tr, tf, ts, tc);
+    } else {
+        const int64_t len = gossip_format_statistics(n, gen.data(), recv.data(), fwd.data(), sent.data(),
+                                                     proc.data(), peers.data(), sock.data(), nullptr, 0);
+        if (len < 0) return die("format");
+        std::string buf((size_t)len + 1, '\0');
+        gossip_format_statistics(n, gen.data(), recv.data(), fwd.data(), sent.data(), proc.data(),
+                                 peers.data(), sock.data(), &buf[0], buf.size());
+        std::fputs(buf.c_str(), stdout);
+    }
+    std::printf("All nodes stopped.\n");
+    gossip_counters c{};
+    gossip_engine_get_counters(eng, &c);
+    std::fprintf(stderr,
+                 "[engine] %llu ticks, %llu edge events in %.3f s wall (%.3e edge events/s), "
+                 "window %u/%u words%s\n",
+                 (unsigned long long)c.ticks, (unsigned long long)c.edge_events, wall,
+                 wall > 0 ? (double)c.edge_events / wall : 0.0, c.words_hw, c.words_cap,
+                 o.timing ? "" : "");
+    if (o.timing && c.pull_ms > 0)
+        std::fprintf(stderr, "[engine] pull kernel %.3f ms over %llu launches, %.1f GB/s algorithmic\n",
+                     c.pull_ms, (unsigned long long)c.pull_launches, c.pull_bytes / (c.pull_ms * 1e6));
+    gossip_engine_destroy(eng);
+    gossip_schedule_destroy(sched);
+    gossip_topology_destroy(topo);
+    return 0;
+}

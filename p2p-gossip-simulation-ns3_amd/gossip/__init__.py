@@ -1,0 +1,447 @@
+"""Python host mirror of the MI355X gossip engine (ctypes over libgossip.so's C ABI).
+
+The product's host side is C++ (``csrc/gossip_sim.cpp``, like the reference's
+``p2pnetwork.cc``); this module is the thin binding that tests and ``bench.py`` use.  It
+mirrors the reference's ``P2PGossipNetworkSimulation`` (p2pnetwork.cc:15-286) so parity
+tests read like the reference's own program:
+
+    sim = P2PGossipNetworkSimulation(numNodes)          # p2pnetwork.cc:40-50
+    sim.CreateRandomTopology(connectionProbability, latency)   # :62-96
+    sim.Start(simulationTime)                           # :193-218
+    sim.PrintStatistics()                               # :253-285
+
+There is no CPU fallback: every call goes through ``libgossip.so`` and the engine refuses to
+start without a HIP device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(os.path.dirname(_HERE), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libgossip.so")
+
+TOPO_EXACT = 0
+TOPO_SKIP = 1
+MODE_AUTO = 0
+MODE_CSR = 1
+F_TRACE = 1
+F_TIMING = 2
+
+EXPORTED_SYMBOLS = (
+    "gossip_last_error", "gossip_version", "gossip_seconds_to_ns", "gossip_milliseconds_to_ns",
+    "gossip_topology_create", "gossip_topology_from_links", "gossip_topology_num_nodes",
+    "gossip_topology_num_links", "gossip_topology_get_links", "gossip_topology_num_entries",
+    "gossip_topology_get_csr", "gossip_topology_get_degrees", "gossip_topology_destroy",
+    "gossip_schedule_create", "gossip_schedule_from_events", "gossip_schedule_size",
+    "gossip_schedule_get", "gossip_schedule_destroy", "gossip_shard_events",
+    "gossip_engine_create", "gossip_engine_set_graph", "gossip_engine_set_topology",
+    "gossip_engine_set_schedule", "gossip_engine_set_schedule_obj", "gossip_engine_add_snapshot",
+    "gossip_engine_first_tick", "gossip_engine_end_tick", "gossip_engine_current_tick",
+    "gossip_engine_run", "gossip_engine_sync", "gossip_engine_get_stats",
+    "gossip_engine_get_snapshot", "gossip_engine_get_counters", "gossip_engine_reset_timing",
+    "gossip_engine_trace_size", "gossip_engine_get_trace", "gossip_engine_destroy",
+    "gossip_format_statistics", "gossip_format_periodic",
+)
+
+GEN_EVENT_DTYPE = np.dtype([("ns", "<i8"), ("node", "<u4"), ("share_id", "<u4")])
+
+
+class GossipError(RuntimeError):
+    pass
+
+
+class gossip_config(C.Structure):
+    _fields_ = [
+        ("num_nodes", C.c_uint32), ("latency_ns", C.c_int64), ("t_start_ns", C.c_int64),
+        ("t_cut_ns", C.c_int64), ("device", C.c_int32), ("mode", C.c_int32),
+        ("max_words", C.c_uint32), ("shard_rank", C.c_uint32), ("shard_count", C.c_uint32),
+        ("flags", C.c_uint32),
+    ]
+
+
+class gossip_counters(C.Structure):
+    _fields_ = [
+        ("edge_events", C.c_uint64), ("receptions", C.c_uint64), ("generations", C.c_uint64),
+        ("ticks", C.c_uint64), ("pull_launches", C.c_uint64), ("pull_ms", C.c_double),
+        ("pull_bytes", C.c_uint64), ("words_hw", C.c_uint32), ("words_cap", C.c_uint32),
+        ("device_bytes", C.c_uint64),
+    ]
+
+
+_lib = None
+
+
+def _ptr(a, ct):
+    return a.ctypes.data_as(C.POINTER(ct)) if a is not None else None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libgossip.so (build it with ``__graft_entry__.build()``); raise if missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise GossipError(f"{path} not built: run __graft_entry__.build() (no CPU fallback)")
+    lib = C.CDLL(path)
+    P, u32, u64, i64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int64, C.c_int32
+    sig = {
+        "gossip_last_error": (C.c_char_p, []),
+        "gossip_version": (C.c_char_p, []),
+        "gossip_seconds_to_ns": (i64, [C.c_double]),
+        "gossip_milliseconds_to_ns": (i64, [C.c_double]),
+        "gossip_topology_create": (C.c_int, [u32, C.c_double, u32, C.c_int, C.c_int, C.POINTER(P)]),
+        "gossip_topology_from_links": (C.c_int, [u32, u64, P, P, C.POINTER(P)]),
+        "gossip_topology_num_nodes": (u32, [P]),
+        "gossip_topology_num_links": (u64, [P]),
+        "gossip_topology_get_links": (C.c_int, [P, P, P]),
+        "gossip_topology_num_entries": (u64, [P]),
+        "gossip_topology_get_csr": (C.c_int, [P, P, P, P]),
+        "gossip_topology_get_degrees": (C.c_int, [P, P, P]),
+        "gossip_topology_destroy": (None, [P]),
+        "gossip_schedule_create": (C.c_int, [u32, u32, i64, i64, i64, u32, C.c_int, C.POINTER(P)]),
+        "gossip_schedule_from_events": (C.c_int, [u64, P, C.POINTER(P)]),
+        "gossip_schedule_size": (u64, [P]),
+        "gossip_schedule_get": (C.c_int, [P, P]),
+        "gossip_schedule_destroy": (None, [P]),
+        "gossip_shard_events": (C.c_int, [P, u64, P, u32, P]),
+        "gossip_engine_create": (C.c_int, [C.POINTER(gossip_config), C.POINTER(P)]),
+        "gossip_engine_set_graph": (C.c_int, [P, u32, P, P, P]),
+        "gossip_engine_set_topology": (C.c_int, [P, P]),
+        "gossip_engine_set_schedule": (C.c_int, [P, u64, P]),
+        "gossip_engine_set_schedule_obj": (C.c_int, [P, P]),
+        "gossip_engine_add_snapshot": (C.c_int, [P, i64]),
+        "gossip_engine_first_tick": (i64, [P]),
+        "gossip_engine_end_tick": (i64, [P]),
+        "gossip_engine_current_tick": (i64, [P]),
+        "gossip_engine_run": (C.c_int, [P, i64]),
+        "gossip_engine_sync": (C.c_int, [P]),
+        "gossip_engine_get_stats": (C.c_int, [P, P, P, P, P, P, P, P]),
+        "gossip_engine_get_snapshot": (C.c_int, [P, u32, P, P, P]),
+        "gossip_engine_get_counters": (C.c_int, [P, C.POINTER(gossip_counters)]),
+        "gossip_engine_reset_timing": (C.c_int, [P]),
+        "gossip_engine_trace_size": (u64, [P]),
+        "gossip_engine_get_trace": (C.c_int, [P, P, P, P, P, P]),
+        "gossip_engine_destroy": (None, [P]),
+        "gossip_format_statistics": (i64, [u32, P, P, P, P, P, P, P, C.c_char_p, u64]),
+        "gossip_format_periodic": (i64, [C.c_double, u32, u64, u64, u64, C.c_char_p, u64]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise GossipError(f"{what}: {load_library().gossip_last_error().decode()} (code {rc})")
+
+
+def _vp(a):
+    return C.c_void_p(a.ctypes.data) if a is not None and a.size else None
+
+
+def seconds_to_ns(s: float) -> int:
+    return int(load_library().gossip_seconds_to_ns(float(s)))
+
+
+def milliseconds_to_ns(ms: float) -> int:
+    return int(load_library().gossip_milliseconds_to_ns(float(ms)))
+
+
+class Topology:
+    """G(n,p) link set with the reference's fix-up (p2pnetwork.cc:62-96) and its peer lists."""
+
+    def __init__(self, handle):
+        self._h = C.c_void_p(handle)
+
+    @classmethod
+    def gnp(cls, n: int, p: float, seed: int, kind: int = TOPO_EXACT, threads: int = 8):
+        lib = load_library()
+        h = C.c_void_p()
+        _check(lib.gossip_topology_create(n, p, seed, kind, threads, C.byref(h)), "topology")
+        return cls(h.value)
+
+    @classmethod
+    def from_links(cls, n: int, a, b):
+        lib = load_library()
+        a = np.ascontiguousarray(a, dtype=np.uint32)
+        b = np.ascontiguousarray(b, dtype=np.uint32)
+        h = C.c_void_p()
+        _check(lib.gossip_topology_from_links(n, a.size, _vp(a), _vp(b), C.byref(h)), "topology")
+        return cls(h.value)
+
+    @property
+    def num_nodes(self) -> int:
+        return int(load_library().gossip_topology_num_nodes(self._h))
+
+    def links(self):
+        lib = load_library()
+        m = int(lib.gossip_topology_num_links(self._h))
+        a = np.empty(m, np.uint32)
+        b = np.empty(m, np.uint32)
+        _check(lib.gossip_topology_get_links(self._h, _vp(a), _vp(b)), "links")
+        return a, b
+
+    def csr(self):
+        lib = load_library()
+        n = self.num_nodes
+        nnz = int(lib.gossip_topology_num_entries(self._h))
+        rp = np.empty(n + 1, np.int64)
+        col = np.empty(nnz, np.int32)
+        mult = np.empty(nnz, np.uint8)
+        _check(lib.gossip_topology_get_csr(self._h, _vp(rp), _vp(col), _vp(mult)), "csr")
+        return rp, col, mult
+
+    def degrees(self):
+        lib = load_library()
+        n = self.num_nodes
+        peers = np.empty(n, np.uint32)
+        sockets = np.empty(n, np.uint32)
+        _check(lib.gossip_topology_get_degrees(self._h, _vp(peers), _vp(sockets)), "degrees")
+        return peers, sockets
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.gossip_topology_destroy(self._h)
+            self._h = None
+
+
+def make_schedule(n: int, node_seed: int, t_start_ns: int, t_cut_ns: int, t_gen_end_ns: int = 0,
+                  id_mask: int = 0, threads: int = 8) -> np.ndarray:
+    """Counted share generations (p2pnode.cc:91-125, 201-209) as a GEN_EVENT_DTYPE array."""
+    lib = load_library()
+    h = C.c_void_p()
+    _check(lib.gossip_schedule_create(n, node_seed, t_start_ns, t_cut_ns, t_gen_end_ns, id_mask,
+                                      threads, C.byref(h)), "schedule")
+    try:
+        m = int(lib.gossip_schedule_size(h))
+        ev = np.empty(m, GEN_EVENT_DTYPE)
+        if m:
+            _check(lib.gossip_schedule_get(h, _vp(ev)), "schedule get")
+        return ev
+    finally:
+        lib.gossip_schedule_destroy(h)
+
+
+def shard_events(topo: "Topology", ev: np.ndarray, shard_count: int) -> np.ndarray:
+    """Owner shard of every generation event (the engines' multi-GPU sharding rule)."""
+    ev = np.ascontiguousarray(ev, GEN_EVENT_DTYPE)
+    owner = np.empty(ev.size, np.uint32)
+    _check(load_library().gossip_shard_events(topo._h, ev.size, _vp(ev), shard_count, _vp(owner)),
+           "shard events")
+    return owner
+
+
+def events_from_arrays(ns, node, share_id) -> np.ndarray:
+    ev = np.empty(len(ns), GEN_EVENT_DTYPE)
+    ev["ns"] = ns
+    ev["node"] = node
+    ev["share_id"] = share_id
+    return ev
+
+
+@dataclass
+class Stats:
+    gen: np.ndarray
+    recv: np.ndarray
+    fwd: np.ndarray
+    sent: np.ndarray
+    processed: np.ndarray
+    peers: np.ndarray
+    sockets: np.ndarray
+
+
+class Engine:
+    """The tick-synchronous HIP engine (one tick = Latency)."""
+
+    def __init__(self, num_nodes: int, latency_ns: int, t_start_ns: int, t_cut_ns: int,
+                 device: int = 0, mode: int = MODE_AUTO, max_words: int = 0, shard_rank: int = 0,
+                 shard_count: int = 1, flags: int = 0):
+        lib = load_library()
+        cfg = gossip_config(num_nodes, latency_ns, t_start_ns, t_cut_ns, device, mode, max_words,
+                            shard_rank, shard_count, flags)
+        h = C.c_void_p()
+        _check(lib.gossip_engine_create(C.byref(cfg), C.byref(h)), "engine create")
+        self._h = h
+        self.n = num_nodes
+
+    def set_topology(self, topo: Topology):
+        _check(load_library().gossip_engine_set_topology(self._h, topo._h), "set topology")
+
+    def set_graph(self, row_ptr, col, mult=None):
+        row_ptr = np.ascontiguousarray(row_ptr, np.int64)
+        col = np.ascontiguousarray(col, np.int32)
+        mult = None if mult is None else np.ascontiguousarray(mult, np.uint8)
+        _check(load_library().gossip_engine_set_graph(self._h, self.n, _vp(row_ptr), _vp(col),
+                                                      _vp(mult)), "set graph")
+
+    def add_snapshot(self, t_ns: int):
+        _check(load_library().gossip_engine_add_snapshot(self._h, int(t_ns)), "snapshot")
+
+    def set_schedule(self, ev: np.ndarray):
+        ev = np.ascontiguousarray(ev, GEN_EVENT_DTYPE)
+        _check(load_library().gossip_engine_set_schedule(self._h, ev.size, _vp(ev)), "set schedule")
+
+    @property
+    def first_tick(self) -> int:
+        return int(load_library().gossip_engine_first_tick(self._h))
+
+    @property
+    def end_tick(self) -> int:
+        return int(load_library().gossip_engine_end_tick(self._h))
+
+    @property
+    def current_tick(self) -> int:
+        return int(load_library().gossip_engine_current_tick(self._h))
+
+    def run(self, tick_end: int | None = None):
+        if tick_end is None:
+            tick_end = self.end_tick
+        _check(load_library().gossip_engine_run(self._h, int(tick_end)), "run")
+
+    def sync(self):
+        _check(load_library().gossip_engine_sync(self._h), "sync")
+
+    def stats(self) -> Stats:
+        n = self.n
+        a = [np.empty(n, np.uint32) for _ in range(3)]
+        sent = np.empty(n, np.uint64)
+        b = [np.empty(n, np.uint32) for _ in range(3)]
+        _check(load_library().gossip_engine_get_stats(self._h, _vp(a[0]), _vp(a[1]), _vp(a[2]),
+                                                      _vp(sent), _vp(b[0]), _vp(b[1]), _vp(b[2])),
+               "stats")
+        return Stats(a[0], a[1], a[2], sent, b[0], b[1], b[2])
+
+    def snapshot(self, k: int):
+        t = C.c_int64()
+        g = C.c_uint64()
+        p = C.c_uint64()
+        _check(load_library().gossip_engine_get_snapshot(self._h, k, C.byref(t), C.byref(g),
+                                                         C.byref(p)), "snapshot")
+        return t.value, g.value, p.value
+
+    def counters(self) -> gossip_counters:
+        c = gossip_counters()
+        _check(load_library().gossip_engine_get_counters(self._h, C.byref(c)), "counters")
+        return c
+
+    def reset_timing(self):
+        _check(load_library().gossip_engine_reset_timing(self._h), "reset timing")
+
+    def trace(self):
+        lib = load_library()
+        m = int(lib.gossip_engine_trace_size(self._h))
+        node = np.empty(m, np.uint32)
+        sid = np.empty(m, np.uint32)
+        tick = np.empty(m, np.int64)
+        hop = np.empty(m, np.uint32)
+        via = np.empty(m, np.uint8)
+        if m:
+            _check(lib.gossip_engine_get_trace(self._h, _vp(node), _vp(sid), _vp(tick), _vp(hop),
+                                               _vp(via)), "trace")
+        return node, sid, tick, hop, via
+
+    def close(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.gossip_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+def format_statistics(st: Stats) -> str:
+    lib = load_library()
+    n = st.gen.size
+    args = [_vp(np.ascontiguousarray(x)) for x in
+            (st.gen, st.recv, st.fwd, st.sent, st.processed, st.peers, st.sockets)]
+    ln = lib.gossip_format_statistics(n, *args, None, 0)
+    buf = C.create_string_buffer(ln + 1)
+    lib.gossip_format_statistics(n, *args, buf, ln + 1)
+    return buf.value.decode()
+
+
+def format_periodic(t_seconds: float, n: int, total_gen: int, total_processed: int,
+                    total_sockets: int) -> str:
+    lib = load_library()
+    ln = lib.gossip_format_periodic(t_seconds, n, total_gen, total_processed, total_sockets, None, 0)
+    buf = C.create_string_buffer(ln + 1)
+    lib.gossip_format_periodic(t_seconds, n, total_gen, total_processed, total_sockets, buf, ln + 1)
+    return buf.value.decode()
+
+
+class P2PGossipNetworkSimulation:
+    """Mirror of the reference class (p2pnetwork.cc:15-286) driving the HIP engine.
+
+    ``rd()`` is replaced by explicit seeds: ``topo_seed`` (p2pnetwork.cc:65) and
+    ``node_seed`` (node i seeds ``node_seed + i``, p2pnode.cc:41).
+    """
+
+    def __init__(self, numNodes: int, topo_seed: int = 1, node_seed: int = 1000, device: int = 0,
+                 topology_kind: int | None = None, threads: int = 8, flags: int = 0):
+        if numNodes < 2:
+            # p2pnetwork.cc:82 calls nodes.Get(1) for the fix-up of row 0: out of range.
+            raise GossipError("numNodes < 2: the reference's topology fix-up aborts")
+        self.numNodes = numNodes
+        self.topo_seed = topo_seed
+        self.node_seed = node_seed
+        self.device = device
+        self.kind = topology_kind
+        self.threads = threads
+        self.flags = flags
+        self.topology = None
+        self.latency_ns = None
+        self.engine = None
+        self.periodic = []
+        self.stats = None
+
+    def CreateRandomTopology(self, connectionProbability: float = 0.3, latency: float = 5.0):
+        kind = self.kind
+        if kind is None:
+            kind = TOPO_EXACT if self.numNodes <= 16384 else TOPO_SKIP
+        self.topology = Topology.gnp(self.numNodes, connectionProbability, self.topo_seed, kind,
+                                     self.threads)
+        self.latency_ns = milliseconds_to_ns(latency)
+
+    def Start(self, simulationTime: float = 100.0, statsInterval: float = 10.0):
+        if self.topology is None:
+            raise GossipError("CreateRandomTopology first")
+        t_start = seconds_to_ns(5.0)
+        t_cut = seconds_to_ns(simulationTime - 0.1)
+        ev = make_schedule(self.numNodes, self.node_seed, t_start, t_cut, threads=self.threads)
+        eng = Engine(self.numNodes, self.latency_ns, t_start, t_cut, device=self.device,
+                     flags=self.flags)
+        eng.set_topology(self.topology)
+        times = []
+        t = statsInterval
+        while t < simulationTime:
+            times.append(t)
+            eng.add_snapshot(seconds_to_ns(t))
+            t += statsInterval
+        eng.set_schedule(ev)
+        eng.run()
+        eng.sync()
+        self.engine = eng
+        self.stats = eng.stats()
+        if t_cut < t_start:
+            self.stats.peers[:] = 0
+            self.stats.sockets[:] = 0
+        total_sock = int(self.topology.degrees()[1].sum())
+        self.periodic = []
+        for k, ts in enumerate(times):
+            tns, g, p = eng.snapshot(k)
+            self.periodic.append((ts, g, p, total_sock if tns >= t_start else 0))
+        return self.stats
+
+    def PrintPeriodicStats(self) -> str:
+        return "".join(format_periodic(t, self.numNodes, g, p, s) for t, g, p, s in self.periodic)
+
+    def PrintStatistics(self) -> str:
+        return format_statistics(self.stats)
