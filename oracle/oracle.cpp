@@ -404,9 +404,26 @@ int oracle_run(oracle_sim* s) {
             case EV_STATS: break;
         }
         if (e.type == EV_STATS) {
-            // StopAllNodes (same time, scheduled after PrintStatistics): nothing after
-            // this point is observable in the report.
+            // StopAllNodes (same time, scheduled after PrintStatistics) stops generation and
+            // closes every socket (p2pnode.cc:55-69: peersockets.clear()).  Only periodic
+            // stats scheduled in (t_cut, simTime) can still print; they see the counters
+            // frozen at t_cut and zero socket connections (arrivals at closed sockets are
+            // not delivered to HandleRead).
             s->on_stats();
+            while (!s->q.empty()) {
+                const Event r = s->q.top();
+                s->q.pop();
+                if (r.type != EV_PERIODIC) continue;
+                uint32_t tg = 0, tp = 0;
+                for (const Node& nd : s->nodes) {
+                    tg += nd.gen;
+                    tp += (uint32_t)nd.processed.size();
+                }
+                s->per_t.push_back(r.t);
+                s->per_gen.push_back(tg);
+                s->per_proc.push_back(tp);
+                s->per_sock.push_back(0);
+            }
             break;
         }
     }

@@ -1067,14 +1067,27 @@ int gossip_engine_get_snapshot(gossip_engine* e, uint32_t k, int64_t* t_ns, uint
     if (!e || k >= e->snaps.size()) return set_error(GOSSIP_EINVAL, "bad snapshot index");
     if (!e->have_sched) return set_error(GOSSIP_ESTATE, "no schedule");
     const auto& s = e->snaps[k];
+    HIP_TRY(hipSetDevice(e->device));
+    if (t_ns) *t_ns = s.t_ns;
+    if (total_gen) *total_gen = s.gen_total;
+    if (s.t_ns > e->cfg.t_cut_ns) {
+        // After PrintStatistics + StopAllNodes: counters frozen at t_cut (the caller reports
+        // zero socket connections, p2pnode.cc:55-69).
+        if (e->cur < e->tick_end) return set_error(GOSSIP_ESTATE, "snapshot after t_cut needs the full run");
+        HIP_TRY(hipMemsetAsync(e->d_scalars, 0, 8, e->stream));
+        k_sum_u32<<<256, 256, 0, e->stream>>>(e->d_recv, e->d_effgen, e->n, e->d_scalars);
+        HIP_TRY(hipGetLastError());
+        unsigned long long v = 0;
+        HIP_TRY(hipMemcpyAsync(&v, e->d_scalars, 8, hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        if (total_processed) *total_processed = v;
+        return GOSSIP_OK;
+    }
     if (e->cur <= s.tick - (s.r ? 0 : 1) && s.tick >= e->tick0)
         return set_error(GOSSIP_ESTATE, "snapshot time not simulated yet");
-    HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
     unsigned long long v[2] = {0, 0};
     HIP_TRY(hipMemcpy(v, e->d_scalars + 2 + 2 * k, 16, hipMemcpyDeviceToHost));
-    if (t_ns) *t_ns = s.t_ns;
-    if (total_gen) *total_gen = s.gen_total;
     if (total_processed) *total_processed = (s.tick <= e->tick0 && s.r == 0) ? 0 : (v[0] + v[1]);
     return GOSSIP_OK;
 }

@@ -219,7 +219,8 @@ int main(int argc, char** argv) {
         int64_t tns;
         uint64_t tg, tp;
         if (gossip_engine_get_snapshot(eng, (uint32_t)k, &tns, &tg, &tp)) return die("snapshot read");
-        const uint64_t sockets_now = tns >= t_start ? total_sock : 0;
+        // sockets exist from makeconnections (t_start) until StopAllNodes (t_cut)
+        const uint64_t sockets_now = (tns >= t_start && tns <= t_cut) ? total_sock : 0;
         std::string buf((size_t)gossip_format_periodic(per_t[k], n, tg, tp, sockets_now, nullptr, 0) + 1, '\0');
         gossip_format_periodic(per_t[k], n, tg, tp, sockets_now, &buf[0], buf.size());
         std::fputs(buf.c_str(), stdout);

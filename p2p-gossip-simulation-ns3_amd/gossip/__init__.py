@@ -437,7 +437,9 @@ class P2PGossipNetworkSimulation:
         self.periodic = []
         for k, ts in enumerate(times):
             tns, g, p = eng.snapshot(k)
-            self.periodic.append((ts, g, p, total_sock if tns >= t_start else 0))
+            # sockets exist from makeconnections (t_start) until StopAllNodes (t_cut)
+            live = t_start <= tns <= t_cut
+            self.periodic.append((ts, g, p, total_sock if live else 0))
         return self.stats
 
     def PrintPeriodicStats(self) -> str:

@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 --kernel-trace --stats run of bench.py for profiles/.
+
+    python tools/prof_summary.py <prof_dir> <run_name> --timed K [--out profiles/x.json]
+
+Reports every kernel's call count / average duration (from <run>_kernel_stats.csv) and the
+average duration of the LAST K k_pull dispatches (the bench's timed window), which is the
+number bench.py's live HIP-event average must agree with.
+"""
+import argparse
+import csv
+import json
+import os
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof_dir")
+    ap.add_argument("run")
+    ap.add_argument("--timed", type=int, required=True)
+    ap.add_argument("--kernel", default="k_pull")
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    stats = list(csv.DictReader(open(os.path.join(a.prof_dir, f"{a.run}_kernel_stats.csv"))))
+    trace = list(csv.DictReader(open(os.path.join(a.prof_dir, f"{a.run}_kernel_trace.csv"))))
+    pulls = [r for r in trace if a.kernel in r["Kernel_Name"]]
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in pulls]
+    timed = dur[-a.timed:]
+    out = {
+        "kernels": [{"name": r["Name"], "calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
+                     "total_ms": float(r["TotalDurationNs"]) / 1e6, "pct": float(r["Percentage"])}
+                    for r in stats],
+        "timed_kernel": a.kernel,
+        "timed_launches": len(timed),
+        "timed_avg_ms": sum(timed) / max(len(timed), 1),
+        "timed_min_ms": min(timed) if timed else None,
+        "timed_max_ms": max(timed) if timed else None,
+        "vgpr": int(pulls[-1]["VGPR_Count"]) if pulls else None,
+        "sgpr": int(pulls[-1]["SGPR_Count"]) if pulls else None,
+        "lds_bytes": int(pulls[-1]["LDS_Block_Size"]) if pulls else None,
+        "grid": int(pulls[-1]["Grid_Size_X"]) if pulls else None,
+    }
+    s = json.dumps(out, indent=1)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(s + "\n")
+    print(s)
+
+
+if __name__ == "__main__":
+    main()
