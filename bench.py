@@ -36,6 +36,7 @@ import gossip  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 T0_NS = 5_000_000_000
+SLICE_NS = 10_000_000_000  # steady-state slice start (tick 2000 at 5 ms)
 L_NS = 5_000_000
 T_CUT_NS = 59_900_000_000
 
@@ -73,12 +74,12 @@ def cpu_baseline(topo, ev, sample_shares, threads):
 
     a, b = topo.links()
     sub = ev[:sample_shares]
-    r = oracle.run_replay(topo.num_nodes, L_NS, T0_NS, oracle.INT64_MAX, a, b, sub["ns"],
+    r = oracle.run_replay(topo.num_nodes, L_NS, SLICE_NS, oracle.INT64_MAX, a, b, sub["ns"],
                           sub["node"], sub["share_id"])
     return dict(value=r.edge_events / r.wall_s if r.wall_s > 0 else None, unit="edge events/s",
                 cores=1, kind="port",
                 sample=f"ORACLE A (event-driven P2PNode logic, unordered_set seen-sets) on the "
-                       f"same graph, the first {len(sub)} generations after t=5 s, floods run "
+                       f"same graph, the first {len(sub)} generations after t=10 s, floods run "
                        f"to completion: {r.edge_events} edge events in {r.wall_s:.2f} s "
                        f"(host nproc {os.cpu_count()}, threads=1)")
 
@@ -91,6 +92,9 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=2)
+    ap.add_argument("--rehearse-shards", type=int, default=0,
+                    help="diagnostic: run only shard 0 of S on this one GPU (per-rank footprint "
+                         "and time of an S-GPU run); the JSON line is marked REHEARSAL")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -98,24 +102,42 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     n_gpus = args.gpus
     dist = None
+    dev = None
     if world > 1:
         import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")  # RCCL over xGMI
+        # GOSSIP_DIST_BACKEND=gloo + GOSSIP_BENCH_NODES: rehearsal of N ranks on one GPU.
+        backend = os.environ.get("GOSSIP_DIST_BACKEND", "nccl")  # "nccl" = RCCL over xGMI
+        local = local % max(torch.cuda.device_count(), 1)
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dev = f"cuda:{local}"
+        dist.init_process_group(backend)
+        import gossip.dist as gd
     wl = workload(n_gpus)
+    if os.environ.get("GOSSIP_BENCH_NODES"):
+        wl["nodes"] = int(os.environ["GOSSIP_BENCH_NODES"])
+        wl["desc"] += f" [REHEARSAL: {wl['nodes']} nodes]"
     n = wl["nodes"]
     p = 16.0 / (n - 1)
     W, K = args.warmup, args.steps
 
     t_setup = time.time()
     topo = gossip.Topology.gnp(n, p, wl["topo_seed"], gossip.TOPO_SKIP, threads=args.threads)
-    t_gen_end = T0_NS + (W + K + 1) * L_NS
+    # Steady-state slice: the share schedule is the reference's (node RNGs from t = 0, ids
+    # counted from t = 5 s); the slice starts at t = 10 s (tick 2000), where the U(2,5) s
+    # renewal density has settled at 1/3.5 s per node (at t = 5 s it is only 1/9 s).
+    t_gen_end = SLICE_NS + (W + K + 1) * L_NS
     ev = gossip.make_schedule(n, wl["node_seed"], T0_NS, T_CUT_NS, t_gen_end_ns=t_gen_end,
                               threads=args.threads)
-    eng = gossip.Engine(n, L_NS, T0_NS, T_CUT_NS, device=local, flags=gossip.F_TIMING,
-                        shard_rank=rank, shard_count=max(world, 1))
+    ev = ev[ev["ns"] >= SLICE_NS]
+    shards = max(world, 1)
+    if args.rehearse_shards > 1 and world == 1:
+        shards = args.rehearse_shards
+        wl["desc"] += f" [REHEARSAL: shard 0 of {shards} on one GPU]"
+    eng = gossip.Engine(n, L_NS, SLICE_NS, T_CUT_NS, device=local, flags=gossip.F_TIMING,
+                        shard_rank=rank, shard_count=shards)
     eng.set_topology(topo)
     eng.set_schedule(ev)
     if rank == 0:
@@ -141,25 +163,26 @@ def main():
     c1 = eng.counters()
     edges = c1.edge_events - c0.edge_events
     pull_ms, pull_bytes, launches = c1.pull_ms, c1.pull_bytes, c1.pull_launches
+    gens_done = c1.generations
     if dist:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        s = torch.tensor([edges, pull_bytes], dtype=torch.float64, device="cuda")
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        edges_total = int(s[0].item())
-        m = torch.tensor([pull_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(m, op=dist.ReduceOp.MAX)
-        pull_ms_max = float(m.item())
+        elapsed, pull_ms_max = gd.allreduce_scalars([elapsed, pull_ms], op="max", device=dev)
+        edges_total, gens_total = gd.allreduce_scalars([edges, gens_done], op="sum", device=dev)
+        edges_total = int(edges_total)
+        # every counted generation of the simulated ticks ran on exactly one rank
+        want = int(np.count_nonzero(ev["ns"] < (tick0 + W + K) * L_NS))
+        if int(gens_total) != want:
+            raise SystemExit(f"shard coverage broken: {int(gens_total)} generations vs {want}")
     else:
         edges_total = edges
         pull_ms_max = pull_ms
 
     if rank == 0:
         avg_ms = pull_ms / max(launches, 1)
-        bytes_per_launch = pull_bytes / max(launches, 1)
+        # Algorithmic bytes per launch of the implemented pull: 16 B per
+        # (edge, word-pair) neighbour read actually needed + 4 B per col index of a pulling
+        # node pass + 16 B per own-row seen/F access + 24 B of per-node row_ptr/counters.
+        bytes_per_launch = c1.pull_bytes_moved / max(launches, 1)
+        dense_bytes_per_launch = pull_bytes / max(launches, 1)  # SURVEY §8d dense formula
         achieved = bytes_per_launch / (avg_ms * 1e6) if avg_ms > 0 else 0.0  # GB/s
         traffic = pmc_traffic(wl["name"], n_gpus)
         out = {
@@ -184,7 +207,9 @@ def main():
                 "ticks_timed": [tick0 + W, tick0 + W + K],
                 "edge_events_timed": edges_total,
                 "live_words_per_node": c1.words_hw,
-                "parallelism": f"share-shard x{max(world, 1)}",
+                "window_capacity_words": c1.words_cap,
+                "device_gib": c1.device_bytes / 2**30,
+                "parallelism": f"share-shard x{shards}",
             },
             "roofline": {
                 "bound": "hbm",
@@ -195,6 +220,8 @@ def main():
                 "traffic": traffic,
                 "kernel": "k_pull",
                 "bytes_per_launch": bytes_per_launch,
+                "dense_formula_bytes_per_launch": dense_bytes_per_launch,
+                "dense_formula_equiv_gbs": (dense_bytes_per_launch / (avg_ms * 1e6)) if avg_ms > 0 else None,
                 "avg_launch_ms": avg_ms,
                 "pull_fraction_of_step": (pull_ms_max / (elapsed * 1e3)) if elapsed > 0 else None,
             },

@@ -173,10 +173,14 @@ typedef struct gossip_counters {
     uint64_t ticks;            /* ticks simulated                                   */
     uint64_t pull_launches;    /* pull-kernel launches                              */
     double pull_ms;            /* summed HIP-event time of pull launches (TIMING)   */
-    uint64_t pull_bytes;       /* algorithmic bytes of those launches   */
+    uint64_t pull_bytes;       /* SURVEY 8d dense-pull bytes of those launches:
+                                  8(n+1) + 4nnz + 8*Wq*nnz + 24*Wq*n + 16n each       */
     uint32_t words_hw;         /* high-water frontier words per node                */
     uint32_t words_cap;        /* frontier capacity (words per node)                */
     uint64_t device_bytes;     /* device memory held by the engine                  */
+    uint64_t pull_bytes_moved; /* bytes the pull kernels actually had to move after
+                                  dead-word / saturated-node skipping (since reset)   */
+    uint64_t pull_pair_edges;  /* (edge, 16-B word pair) neighbour reads (since reset) */
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 int gossip_engine_reset_timing(gossip_engine* e);

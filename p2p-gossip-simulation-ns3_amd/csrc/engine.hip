@@ -31,6 +31,7 @@
 #include <numeric>
 #include <queue>
 #include <string>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -76,11 +77,15 @@ struct PullArgs {
     const uint64_t* Fcur;
     uint64_t* Fnext;
     uint64_t* seen;
-    const WordCtl* ctl;
+    const WordCtl* ctl;     // masks, read only for words whose wflags say so
+    const uint8_t* wflags;  // per word: WF_CLEAR | WF_GROUP | WF_KEEP | WF_SNAP
     uint32_t* recv;
     uint64_t* sent;
-    unsigned long long* live;
-    unsigned long long* snap;  // nullable
+    unsigned long long* live;             // liveness of this tick (OR of F_next words)
+    const unsigned long long* live_prev;  // liveness of tick t-1 (nullable: all live)
+    const unsigned long long* live_pp;    // liveness of tick t-2 (nullable: all dirty)
+    unsigned long long* snap;             // nullable
+    unsigned long long* acct;             // traffic accounting (nullable)
     uint32_t n;
     uint32_t stride;
     uint32_t wact;
@@ -109,93 +114,36 @@ __device__ __forceinline__ uint64_t group_fix(uint64_t nw, uint64_t seen, uint64
     return nw;
 }
 
-// LPN = lanes per node (power of two).  Each lane owns two consecutive words (16 B) of a
-// 2*LPN-word pass; neighbour rows are read as 16-B vectors so a 64-lane group reads 1 KiB
-// of one row per instruction.  Several nodes share a wave when the live window is narrow.
-template <int LPN>
-__global__ __launch_bounds__(256) void k_pull(PullArgs a) {
-    constexpr int NPB = 256 / LPN;
-    extern __shared__ unsigned long long s_live[];
-    if (a.use_lds) {
-        for (uint32_t i = threadIdx.x; i < a.wact; i += 256) s_live[i] = 0ull;
-        __syncthreads();
+#include "pull_kernel.h"
+
+template <int LPW, int EPN>
+void launch_pull_t(uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
+    if constexpr (LPW * EPN <= 64) k_pull<LPW, EPN><<<grid, 256, lds, s>>>(a);
+}
+
+template <int LPW>
+void launch_pull_e(int epn, uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
+    switch (epn) {
+        case 1: launch_pull_t<LPW, 1>(grid, lds, s, a); break;
+        case 2: launch_pull_t<LPW, 2>(grid, lds, s, a); break;
+        case 4: launch_pull_t<LPW, 4>(grid, lds, s, a); break;
+        case 8: launch_pull_t<LPW, 8>(grid, lds, s, a); break;
+        case 16: launch_pull_t<LPW, 16>(grid, lds, s, a); break;
+        case 32: launch_pull_t<LPW, 32>(grid, lds, s, a); break;
+        default: launch_pull_t<LPW, 64>(grid, lds, s, a); break;
     }
-    const uint32_t sub = threadIdx.x % LPN;
-    const uint32_t slot = threadIdx.x / LPN;
-    const uint64_t stride = a.stride;
-    unsigned long long snap_local = 0ull;
-    for (uint64_t vb = (uint64_t)blockIdx.x * NPB; vb < a.n; vb += (uint64_t)gridDim.x * NPB) {
-        const uint64_t v = vb + slot;
-        if (v >= a.n) continue;  // uniform across the LPN lanes of a node
-        const int64_t beg = a.rowptr[v], end = a.rowptr[v + 1];
-        uint32_t cnt = 0;
-        for (uint32_t base = 0; base < a.wact; base += 2 * LPN) {
-            const uint32_t w = base + 2 * sub;
-            if (w >= a.wact) continue;
-            const uint64_t* Fw = a.Fcur + w;
-            uint64_t acc0 = 0ull, acc1 = 0ull;
-            int64_t j = beg;
-            for (; j + 4 <= end; j += 4) {
-                const uint64_t u0 = (uint32_t)a.col[j], u1 = (uint32_t)a.col[j + 1];
-                const uint64_t u2 = (uint32_t)a.col[j + 2], u3 = (uint32_t)a.col[j + 3];
-                const ulonglong2 q0 = *reinterpret_cast<const ulonglong2*>(Fw + u0 * stride);
-                const ulonglong2 q1 = *reinterpret_cast<const ulonglong2*>(Fw + u1 * stride);
-                const ulonglong2 q2 = *reinterpret_cast<const ulonglong2*>(Fw + u2 * stride);
-                const ulonglong2 q3 = *reinterpret_cast<const ulonglong2*>(Fw + u3 * stride);
-                acc0 |= (q0.x | q1.x) | (q2.x | q3.x);
-                acc1 |= (q0.y | q1.y) | (q2.y | q3.y);
-            }
-            for (; j < end; j++) {
-                const uint64_t u = (uint32_t)a.col[j];
-                const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(Fw + u * stride);
-                acc0 |= q.x;
-                acc1 |= q.y;
-            }
-            const WordCtl c0 = a.ctl[w], c1 = a.ctl[w + 1];
-            uint64_t* sp = a.seen + v * stride + w;
-            ulonglong2 s = *reinterpret_cast<const ulonglong2*>(sp);
-            s.x &= ~c0.clear;
-            s.y &= ~c1.clear;
-            uint64_t n0 = acc0 & ~s.x & c0.keep;
-            uint64_t n1 = acc1 & ~s.y & c1.keep;
-            if (c0.gmask) n0 = group_fix(n0, s.x, c0.gmask, c0.gstart);
-            if (c1.gmask) n1 = group_fix(n1, s.y, c1.gmask, c1.gstart);
-            if ((n0 | n1 | c0.clear | c1.clear) != 0ull) {
-                s.x |= n0;
-                s.y |= n1;
-                *reinterpret_cast<ulonglong2*>(sp) = s;
-            }
-            ulonglong2 o;
-            o.x = n0;
-            o.y = n1;
-            *reinterpret_cast<ulonglong2*>(a.Fnext + v * stride + w) = o;
-            cnt += (uint32_t)(__popcll(n0) + __popcll(n1));
-            if (a.snap) snap_local += (unsigned long long)(__popcll(n0 & c0.snap) + __popcll(n1 & c1.snap));
-            if (a.use_lds) {
-                if (n0) atomicOr(&s_live[w], (unsigned long long)n0);
-                if (n1) atomicOr(&s_live[w + 1], (unsigned long long)n1);
-            } else {
-                if (n0) atomicOr(&a.live[w], (unsigned long long)n0);
-                if (n1) atomicOr(&a.live[w + 1], (unsigned long long)n1);
-            }
-        }
-#pragma unroll
-        for (int off = LPN / 2; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, LPN);
-        if (sub == 0 && cnt) {
-            a.recv[v] += cnt;
-            a.sent[v] += (uint64_t)cnt * a.deg[v];
-        }
-    }
-    if (a.snap) {
-        for (int off = 32; off > 0; off >>= 1) snap_local += __shfl_xor(snap_local, off, 64);
-        if ((threadIdx.x & 63) == 0 && snap_local) atomicAdd(a.snap, snap_local);
-    }
-    if (a.use_lds) {
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
-            const unsigned long long x = s_live[i];
-            if (x) atomicOr(&a.live[i], x);
-        }
+}
+
+// (LPW, EPN) with LPW * EPN <= 64, both powers of two.
+void launch_pull(int lpw, int epn, uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
+    switch (lpw) {
+        case 1: launch_pull_e<1>(epn, grid, lds, s, a); break;
+        case 2: launch_pull_e<2>(epn, grid, lds, s, a); break;
+        case 4: launch_pull_e<4>(epn, grid, lds, s, a); break;
+        case 8: launch_pull_e<8>(epn, grid, lds, s, a); break;
+        case 16: launch_pull_e<16>(epn, grid, lds, s, a); break;
+        case 32: launch_pull_e<32>(epn, grid, lds, s, a); break;
+        default: launch_pull_e<64>(epn, grid, lds, s, a); break;
     }
 }
 
@@ -291,6 +239,7 @@ struct Instance {
 
 constexpr int kRing = 4;   // host staging slots
 constexpr int kLag = 2;    // ticks of lag before liveness is read back
+constexpr uint32_t kTileWords = 16;  // allocation unit: 16 words = 1024 shares = 128 B per row
 
 }  // namespace
 
@@ -323,13 +272,14 @@ struct gossip_engine {
     uint32_t stride = 0;     // words per node row (capacity, even)
     uint32_t hw = 0;         // high-water words in use (even)
     std::vector<WordCtl> ctl;
-    std::vector<int64_t> last_inject;
-    std::vector<uint8_t> word_alloc;
+    std::vector<uint8_t> tile_alloc;
+    std::vector<int64_t> tile_last_inject;
     std::vector<std::vector<uint32_t>> word_insts;
     std::vector<int32_t> col_phase;     // per column: generation phase (ns % L)
     std::vector<uint32_t> col_src;      // per column: source event index
-    std::priority_queue<uint32_t, std::vector<uint32_t>, std::greater<uint32_t>> free_words;
-    int64_t open_word = -1;
+    std::priority_queue<uint32_t, std::vector<uint32_t>, std::greater<uint32_t>> free_tiles;
+    int64_t open_tile = -1;
+    uint32_t open_word_in_tile = 0;
     uint32_t open_bit = 64;
     std::vector<uint32_t> reset_now;    // words allocated this tick
     // ---- time
@@ -346,9 +296,12 @@ struct gossip_engine {
     uint64_t* d_seen = nullptr;
     uint32_t *d_recv = nullptr, *d_gen = nullptr, *d_effgen = nullptr;
     uint64_t* d_sent = nullptr;
-    unsigned long long* d_live[2] = {nullptr, nullptr};
+    unsigned long long* d_live[3] = {nullptr, nullptr, nullptr};  // liveness ring (tick % 3)
     unsigned long long* d_scalars = nullptr;  // [0]=scratch, [1..]=snapshot base/partial
+    unsigned long long* d_acct = nullptr;     // k_pull traffic accounting (since reset)
     WordCtl* d_ctl[kRing] = {};
+    uint8_t* d_wflags[kRing] = {};
+    uint8_t* h_wflags[kRing] = {};
     Birth* d_births[kRing] = {};
     int32_t* d_gphase[kRing] = {};
     int fcur = 0;
@@ -384,6 +337,8 @@ struct gossip_engine {
     int tick_step(int64_t t);
     int retire_from(int64_t known_tick, const unsigned long long* live);
     int alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t);
+    int grow(uint32_t new_stride);
+    uint32_t grows = 0;
     int decode_trace(int64_t t);
     hipEvent_t get_event();
 };
@@ -399,9 +354,10 @@ gossip_engine::~gossip_engine() {
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
     hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
-    hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_scalars);
+    hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     for (int k = 0; k < kRing; k++) {
-        hipFree(d_ctl[k]); hipFree(d_births[k]); hipFree(d_gphase[k]);
+        hipFree(d_ctl[k]); hipFree(d_births[k]); hipFree(d_gphase[k]); hipFree(d_wflags[k]);
+        hipHostFree(h_wflags[k]);
         hipHostFree(h_ctl[k]); hipHostFree(h_births[k]); hipHostFree(h_gphase[k]);
         hipHostFree(h_live[k]);
         if (slot_done[k]) hipEventDestroy(slot_done[k]);
@@ -566,7 +522,8 @@ int gossip_engine::alloc_device() {
             }
             ecc = std::max(ecc, depth);
         }
-        const int64_t life = ecc + kLag + 4;
+        // (the window widens itself if this is short: gossip_engine::grow)
+        const int64_t life = ecc + kLag + 1;
         const int64_t nt = tick_end - tick0;
         uint64_t peak = 0, run = 0;
         std::vector<uint64_t> cnt((size_t)nt, 0);
@@ -581,11 +538,11 @@ int gossip_engine::alloc_device() {
             if (t >= life) run -= cnt[t - life];
             peak = std::max(peak, run);
         }
-        uint64_t w = (peak + 63) / 64 + (uint64_t)life + 8;  // partial words per tick
+        uint64_t w = (peak + 63) / 64 + 2 * kTileWords;  // + partially filled tiles
         w = (w + 1) & ~1ull;
         words = (uint32_t)std::max<uint64_t>(w, 2);
     }
-    stride = (words + 1) & ~1u;
+    stride = (words + kTileWords - 1) / kTileWords * kTileWords;  // rows start on 128-B lines
     const uint64_t bm = (uint64_t)n * stride * 8;
     size_t freeb = 0, totalb = 0;
     HIP_TRY(hipMemGetInfo(&freeb, &totalb));
@@ -608,17 +565,21 @@ int gossip_engine::alloc_device() {
     HIP_TRY(hipMemsetAsync(d_gen, 0, (size_t)n * 4, stream));
     HIP_TRY(hipMemsetAsync(d_effgen, 0, (size_t)n * 4, stream));
     HIP_TRY(hipMemsetAsync(d_sent, 0, (size_t)n * 8, stream));
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < 3; k++) {
         HIP_TRY(hipMalloc(&d_live[k], (size_t)stride * 8));
         HIP_TRY(hipMemsetAsync(d_live[k], 0, (size_t)stride * 8, stream));
     }
     const size_t nsc = 2 + 2 * snaps.size();
     HIP_TRY(hipMalloc(&d_scalars, nsc * 8));
     HIP_TRY(hipMemsetAsync(d_scalars, 0, nsc * 8, stream));
+    HIP_TRY(hipMalloc(&d_acct, 8 * 8));
+    HIP_TRY(hipMemsetAsync(d_acct, 0, 8 * 8, stream));
     const uint32_t bcap = std::max<uint32_t>(max_births, 1);
     const uint32_t pcap = std::max<uint32_t>(max_group_phases, 1);
     for (int k = 0; k < kRing; k++) {
         HIP_TRY(hipMalloc(&d_ctl[k], (size_t)stride * sizeof(WordCtl)));
+        HIP_TRY(hipMalloc(&d_wflags[k], (size_t)stride + 16));
+        HIP_TRY(hipHostMalloc(&h_wflags[k], (size_t)stride + 16, hipHostMallocDefault));
         HIP_TRY(hipMalloc(&d_births[k], (size_t)bcap * sizeof(Birth)));
         HIP_TRY(hipMalloc(&d_gphase[k], (size_t)pcap * 4));
         HIP_TRY(hipHostMalloc(&h_ctl[k], (size_t)stride * sizeof(WordCtl), hipHostMallocDefault));
@@ -632,8 +593,8 @@ int gossip_engine::alloc_device() {
                    kRing * ((uint64_t)stride * sizeof(WordCtl) + (uint64_t)bcap * sizeof(Birth) + pcap * 4);
     WordCtl z{0ull, ~0ull, 0ull, 0ull, 0ull};
     ctl.assign(stride, z);
-    last_inject.assign(stride, INT64_MIN);
-    word_alloc.assign(stride, 0);
+    tile_alloc.assign(stride / kTileWords, 0);
+    tile_last_inject.assign(stride / kTileWords, INT64_MIN);
     word_insts.assign(stride, {});
     col_phase.assign((size_t)stride * 64, 0);
     col_src.assign((size_t)stride * 64, UINT32_MAX);
@@ -641,45 +602,122 @@ int gossip_engine::alloc_device() {
     return GOSSIP_OK;
 }
 
+// Columns are handed out in TILES of kTileWords words (1024 shares = one 128-B line per node
+// row), so every line of a frontier/seen row holds shares of the same age and the pull's
+// skip decisions are line-coherent.  Births fill the open tile word by word; an id group
+// never straddles a word.
+// Widen every node row to new_stride words (rare: the capacity estimate was short).  Rows are
+// copied with 2-D copies one bitmap at a time so the peak is 3 old + 1 new bitmaps.
+int gossip_engine::grow(uint32_t new_stride) {
+    HIP_TRY(hipStreamSynchronize(stream));
+    const uint64_t nb = (uint64_t)n * new_stride * 8;
+    size_t freeb = 0, totalb = 0;
+    HIP_TRY(hipMemGetInfo(&freeb, &totalb));
+    if (nb + (64ull << 20) > (uint64_t)freeb)
+        return set_error(GOSSIP_ECAPACITY, "live-share window exceeded " + std::to_string(stride) +
+                                               " words per node and there is no device memory to widen it");
+    uint64_t** bufs[3] = {&d_F[0], &d_F[1], &d_seen};
+    for (uint64_t** b : bufs) {
+        uint64_t* nbuf = nullptr;
+        HIP_TRY(hipMalloc(&nbuf, nb));
+        HIP_TRY(hipMemsetAsync(nbuf, 0, nb, stream));
+        HIP_TRY(hipMemcpy2DAsync(nbuf, (size_t)new_stride * 8, *b, (size_t)stride * 8, (size_t)stride * 8, n,
+                                 hipMemcpyDeviceToDevice, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipFree(*b));
+        *b = nbuf;
+    }
+    auto regrow_dev = [&](auto*& p, size_t elem, size_t oldn, size_t newn) -> int {
+        void* q = nullptr;
+        HIP_TRY(hipMalloc(&q, newn * elem));
+        HIP_TRY(hipMemset(q, 0, newn * elem));
+        HIP_TRY(hipMemcpy(q, (const void*)p, oldn * elem, hipMemcpyDeviceToDevice));
+        HIP_TRY(hipFree((void*)p));
+        p = reinterpret_cast<std::remove_reference_t<decltype(p)>>(q);
+        return GOSSIP_OK;
+    };
+    auto regrow_host = [&](auto*& p, size_t elem, size_t oldn, size_t newn) -> int {
+        void* q = nullptr;
+        HIP_TRY(hipHostMalloc(&q, newn * elem, hipHostMallocDefault));
+        std::memset(q, 0, newn * elem);
+        std::memcpy(q, (const void*)p, oldn * elem);
+        HIP_TRY(hipHostFree((void*)p));
+        p = reinterpret_cast<std::remove_reference_t<decltype(p)>>(q);
+        return GOSSIP_OK;
+    };
+    int rc = 0;
+    for (int k = 0; k < 3 && !rc; k++) rc = regrow_dev(d_live[k], 8, stride, new_stride);
+    for (int k = 0; k < kRing && !rc; k++) {
+        rc = regrow_dev(d_ctl[k], sizeof(WordCtl), stride, new_stride);
+        if (!rc) rc = regrow_dev(d_wflags[k], 1, stride + 16, new_stride + 16);
+        if (!rc) rc = regrow_host(h_ctl[k], sizeof(WordCtl), stride, new_stride);
+        if (!rc) rc = regrow_host(h_wflags[k], 1, stride + 16, new_stride + 16);
+        if (!rc) rc = regrow_host(h_live[k], 8, stride, new_stride);
+    }
+    if (rc) return rc;
+    WordCtl z{0ull, ~0ull, 0ull, 0ull, 0ull};
+    ctl.resize(new_stride, z);
+    tile_alloc.resize(new_stride / kTileWords, 0);
+    tile_last_inject.resize(new_stride / kTileWords, INT64_MIN);
+    word_insts.resize(new_stride);
+    col_phase.resize((size_t)new_stride * 64, 0);
+    col_src.resize((size_t)new_stride * 64, UINT32_MAX);
+    device_bytes += 3 * (nb - (uint64_t)n * stride * 8);
+    stride = new_stride;
+    grows++;
+    return GOSSIP_OK;
+}
+
 int gossip_engine::alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t) {
-    if (open_word < 0 || open_bit + k > 64) {
-        uint32_t w;
-        if (!free_words.empty()) {
-            w = free_words.top();
-            free_words.pop();
-        } else {
-            if (hw >= stride)
-                return set_error(GOSSIP_ECAPACITY,
-                                 "live-share window exceeded " + std::to_string(stride) +
-                                     " words per node; raise gossip_config.max_words");
-            w = hw++;
-            if (hw & 1u) {  // keep the processed width even (16-B vectors)
-                if (hw < stride) free_words.push(hw++);
-            }
-        }
-        word_alloc[w] = 1;
-        reset_now.push_back(w);
-        open_word = w;
+    if (open_tile >= 0 && open_bit + k > 64 && open_word_in_tile + 1 < kTileWords) {
+        open_word_in_tile++;
         open_bit = 0;
     }
-    *word = (uint32_t)open_word;
+    if (open_tile < 0 || open_bit + k > 64) {
+        uint32_t tl;
+        if (!free_tiles.empty()) {
+            tl = free_tiles.top();
+            free_tiles.pop();
+        } else {
+            if (hw + kTileWords > stride) {
+                const uint32_t ns = (uint32_t)((stride + stride / 4 + kTileWords) / kTileWords * kTileWords);
+                const int rc = grow(ns);
+                if (rc) return rc;
+            }
+            tl = hw / kTileWords;
+            hw += kTileWords;
+        }
+        tile_alloc[tl] = 1;
+        for (uint32_t q = 0; q < kTileWords; q++) reset_now.push_back(tl * kTileWords + q);
+        open_tile = tl;
+        open_word_in_tile = 0;
+        open_bit = 0;
+    }
+    *word = (uint32_t)open_tile * kTileWords + open_word_in_tile;
     *lo = (uint8_t)open_bit;
     open_bit += k;
-    last_inject[*word] = t;
+    tile_last_inject[(uint32_t)open_tile] = t;
     return GOSSIP_OK;
 }
 
 int gossip_engine::retire_from(int64_t known_tick, const unsigned long long* live) {
-    for (uint32_t w = 0; w < hw; w++) {
-        if (!word_alloc[w] || last_inject[w] > known_tick || live[w] != 0ull) continue;
-        for (uint32_t id : word_insts[w]) inst[id].state = 2;
-        word_insts[w].clear();
-        word_alloc[w] = 0;
-        ctl[w].gmask = 0ull;
-        ctl[w].gstart = 0ull;
-        for (int b = 0; b < 64; b++) col_src[(size_t)w * 64 + b] = UINT32_MAX;
-        free_words.push(w);
-        if ((int64_t)w == open_word) open_word = -1;
+    const uint32_t ntiles = hw / kTileWords;
+    for (uint32_t tl = 0; tl < ntiles; tl++) {
+        if (!tile_alloc[tl] || tile_last_inject[tl] > known_tick) continue;
+        bool any = false;
+        for (uint32_t q = 0; q < kTileWords; q++) any |= live[tl * kTileWords + q] != 0ull;
+        if (any) continue;
+        for (uint32_t q = 0; q < kTileWords; q++) {
+            const uint32_t w = tl * kTileWords + q;
+            for (uint32_t id : word_insts[w]) inst[id].state = 2;
+            word_insts[w].clear();
+            ctl[w].gmask = 0ull;
+            ctl[w].gstart = 0ull;
+            for (int b = 0; b < 64; b++) col_src[(size_t)w * 64 + b] = UINT32_MAX;
+        }
+        tile_alloc[tl] = 0;
+        free_tiles.push(tl);
+        if ((int64_t)tl == open_tile) open_tile = -1;
     }
     return GOSSIP_OK;
 }
@@ -738,7 +776,7 @@ int gossip_engine::tick_step(int64_t t) {
                     col_src[(size_t)w * 64 + l] = (uint32_t)q;
                 }
             }
-            last_inject[I.word] = t;
+            tile_last_inject[I.word / kTileWords] = t;
             b.col = I.word * 64u + I.lo + ev_rank[q];
             if (I.nsrc > 1) {
                 b.kind = BIRTH_GROUP;
@@ -760,6 +798,7 @@ int gossip_engine::tick_step(int64_t t) {
     for (size_t s = 0; s < snaps.size(); s++)
         if (snaps[s].tick == t && snaps[s].r > 0) snap_idx = (int)s;
     WordCtl* C = h_ctl[slot];
+    uint8_t* WF = h_wflags[slot];
     for (uint32_t w = 0; w < hw; w++) {
         WordCtl c = ctl[w];
         if (is_cut || snap_idx >= 0) {
@@ -773,15 +812,18 @@ int gossip_engine::tick_step(int64_t t) {
             if (snap_idx >= 0) c.snap = sm;
         }
         C[w] = c;
+        WF[w] = (uint8_t)((c.clear ? WF_CLEAR : 0u) | (c.gmask ? WF_GROUP : 0u) |
+                          (c.keep != ~0ull ? WF_KEEP : 0u) | (c.snap ? WF_SNAP : 0u));
     }
     for (uint32_t w : reset_now) ctl[w].clear = 0ull;
     // 5. upload + launches
     const uint32_t wact = hw;
     if (wact) HIP_TRY(hipMemcpyAsync(d_ctl[slot], C, (size_t)wact * sizeof(WordCtl), hipMemcpyHostToDevice, stream));
+    if (wact) HIP_TRY(hipMemcpyAsync(d_wflags[slot], WF, (size_t)wact, hipMemcpyHostToDevice, stream));
     if (nb) HIP_TRY(hipMemcpyAsync(d_births[slot], B, (size_t)nb * sizeof(Birth), hipMemcpyHostToDevice, stream));
     if (np) HIP_TRY(hipMemcpyAsync(d_gphase[slot], GP, (size_t)np * 4, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipEventRecord(slot_done[slot], stream));
-    const int lv = (int)(t & 1);
+    const int lv = (int)(t % 3);
     if (wact) HIP_TRY(hipMemsetAsync(d_live[lv], 0, (size_t)wact * 8, stream));
     unsigned long long* snap_ptr = snap_idx >= 0 ? d_scalars + 2 + 2 * snap_idx + 1 : nullptr;
     const int nxt = fcur ^ 1;
@@ -789,14 +831,22 @@ int gossip_engine::tick_step(int64_t t) {
         PullArgs a;
         a.rowptr = d_rowptr; a.col = d_col; a.deg = d_deg;
         a.Fcur = d_F[fcur]; a.Fnext = d_F[nxt]; a.seen = d_seen; a.ctl = d_ctl[slot];
+        a.wflags = d_wflags[slot];
         a.recv = d_recv; a.sent = d_sent; a.live = d_live[lv]; a.snap = snap_ptr;
+        a.live_prev = (t - 1 >= tick0) ? d_live[(t - 1) % 3] : nullptr;
+        a.live_pp = (t - 2 >= tick0) ? d_live[(t - 2) % 3] : nullptr;
+        a.acct = d_acct;
         a.n = n; a.stride = stride; a.wact = wact;
         a.use_lds = wact <= 8192 ? 1u : 0u;
-        int lpn = 1;
-        while (lpn < 64 && 2 * lpn < (int)wact) lpn *= 2;
-        const uint32_t npb = 256 / lpn;
-        const uint64_t groups = ((uint64_t)n + npb - 1) / npb;
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(groups, 2048);
+        // Lane layout: word-lanes cover the window in one pass when possible; spare lanes of
+        // the wave split the peer list (edge-lanes) when peers are many.
+        int lpw = 1;
+        while (lpw < 64 && 2 * lpw < (int)wact) lpw *= 2;
+        int epn = 1;
+        const double avg_deg = n ? (double)nnz / n : 0.0;
+        while (lpw * epn * 2 <= 64 && epn * 8 < avg_deg) epn *= 2;
+        const uint64_t chunks = ((uint64_t)n + 63) / 64;  // 64 nodes per wave step sequence
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, 2048));
         const size_t lds = a.use_lds ? (size_t)wact * 8 : 0;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (cfg.flags & GOSSIP_F_TIMING) {
@@ -804,15 +854,7 @@ int gossip_engine::tick_step(int64_t t) {
             e1 = get_event();
             HIP_TRY(hipEventRecord(e0, stream));
         }
-        switch (lpn) {
-            case 1: k_pull<1><<<grid, 256, lds, stream>>>(a); break;
-            case 2: k_pull<2><<<grid, 256, lds, stream>>>(a); break;
-            case 4: k_pull<4><<<grid, 256, lds, stream>>>(a); break;
-            case 8: k_pull<8><<<grid, 256, lds, stream>>>(a); break;
-            case 16: k_pull<16><<<grid, 256, lds, stream>>>(a); break;
-            case 32: k_pull<32><<<grid, 256, lds, stream>>>(a); break;
-            default: k_pull<64><<<grid, 256, lds, stream>>>(a); break;
-        }
+        launch_pull(lpw, epn, grid, lds, stream, a);
         HIP_TRY(hipGetLastError());
         if (cfg.flags & GOSSIP_F_TIMING) {
             HIP_TRY(hipEventRecord(e1, stream));
@@ -1121,9 +1163,17 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     HIP_TRY(hipGetLastError());
     unsigned long long v[2];
     HIP_TRY(hipMemcpyAsync(v, e->d_scalars, 16, hipMemcpyDeviceToHost, e->stream));
+    unsigned long long acct[8] = {0};
+    HIP_TRY(hipMemcpyAsync(acct, e->d_acct, sizeof(acct), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     c->edge_events = v[0];
     c->receptions = v[1];
+    // Bytes k_pull actually had to move (work-skipping aware): peer-row pairs (16 B),
+    // col indices of the node passes that pulled (4 B), own-row seen reads/writes and F_next
+    // writes (16 B each), row_ptr and the per-node counters.
+    c->pull_bytes_moved = 16ull * acct[0] + 4ull * acct[1] + 16ull * (acct[2] + acct[3] + acct[4]) +
+                          e->pull_launches * (8ull * (e->n + 1) + 16ull * e->n);
+    c->pull_pair_edges = acct[0];
     uint64_t g = 0;
     const uint64_t done = (uint64_t)std::max<int64_t>(0, std::min(e->cur, e->tick_end) - e->tick0);
     if (!e->tick_lo.empty()) g = e->tick_lo[std::min<uint64_t>(done, e->tick_lo.size() - 1)];
@@ -1143,6 +1193,10 @@ int gossip_engine_reset_timing(gossip_engine* e) {
     e->pull_ms_done = 0.0;
     e->pull_launches = 0;
     e->pull_bytes = 0;
+    if (e->d_acct) {
+        HIP_TRY(hipMemsetAsync(e->d_acct, 0, 8 * 8, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+    }
     return GOSSIP_OK;
 }
 

@@ -69,7 +69,8 @@ class gossip_counters(C.Structure):
         ("edge_events", C.c_uint64), ("receptions", C.c_uint64), ("generations", C.c_uint64),
         ("ticks", C.c_uint64), ("pull_launches", C.c_uint64), ("pull_ms", C.c_double),
         ("pull_bytes", C.c_uint64), ("words_hw", C.c_uint32), ("words_cap", C.c_uint32),
-        ("device_bytes", C.c_uint64),
+        ("device_bytes", C.c_uint64), ("pull_bytes_moved", C.c_uint64),
+        ("pull_pair_edges", C.c_uint64),
     ]
 
 
