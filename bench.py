@@ -92,6 +92,8 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=2)
+    ap.add_argument("--noskip", action="store_true",
+                    help="diagnostic: dense pull (every peer-row word read) for PMC calibration")
     ap.add_argument("--rehearse-shards", type=int, default=0,
                     help="diagnostic: run only shard 0 of S on this one GPU (per-rank footprint "
                          "and time of an S-GPU run); the JSON line is marked REHEARSAL")
@@ -136,7 +138,8 @@ def main():
     if args.rehearse_shards > 1 and world == 1:
         shards = args.rehearse_shards
         wl["desc"] += f" [REHEARSAL: shard 0 of {shards} on one GPU]"
-    eng = gossip.Engine(n, L_NS, SLICE_NS, T_CUT_NS, device=local, flags=gossip.F_TIMING,
+    flags = gossip.F_TIMING | (gossip.F_NOSKIP if args.noskip else 0)
+    eng = gossip.Engine(n, L_NS, SLICE_NS, T_CUT_NS, device=local, flags=flags,
                         shard_rank=rank, shard_count=shards)
     eng.set_topology(topo)
     eng.set_schedule(ev)

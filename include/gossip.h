@@ -137,6 +137,8 @@ typedef struct gossip_config {
 
 #define GOSSIP_F_TRACE 1u  /* record first-contact (node, shareId, tick) for tests  */
 #define GOSSIP_F_TIMING 2u /* time each pull-kernel launch with HIP events          */
+#define GOSSIP_F_NOSKIP 4u /* diagnostic: dense pull (no dead/saturated skipping);
+                              results are identical, only the bytes read change       */
 
 int gossip_engine_create(const gossip_config* cfg, gossip_engine** out);
 /* Graph: CSR over distinct neighbours with multiplicity in {1,2} (see topology above). */

@@ -90,6 +90,7 @@ struct PullArgs {
     uint32_t stride;
     uint32_t wact;
     uint32_t use_lds;
+    uint32_t noskip;  // diagnostic: read every peer-row word (dense pull, known byte count)
 };
 
 // Phase-ordered update of id groups inside one word (rare: only words holding groups).
@@ -838,6 +839,7 @@ int gossip_engine::tick_step(int64_t t) {
         a.acct = d_acct;
         a.n = n; a.stride = stride; a.wact = wact;
         a.use_lds = wact <= 8192 ? 1u : 0u;
+        a.noskip = (cfg.flags & GOSSIP_F_NOSKIP) ? 1u : 0u;
         // Lane layout: word-lanes cover the window in one pass when possible; spare lanes of
         // the wave split the peer list (edge-lanes) when peers are many.
         int lpw = 1;

@@ -68,8 +68,8 @@ __device__ __forceinline__ void pull_stage_load(const PullArgs& a, PullStage& st
         const uint16_t fl = *reinterpret_cast<const uint16_t*>(a.wflags + st.w);
         st.f0 = fl & 0xffu;
         st.f1 = fl >> 8;
-        st.lp0 = a.live_prev ? a.live_prev[st.w] : ~0ull;
-        st.lp1 = a.live_prev ? a.live_prev[st.w + 1] : ~0ull;
+        st.lp0 = (a.live_prev && !a.noskip) ? a.live_prev[st.w] : ~0ull;
+        st.lp1 = (a.live_prev && !a.noskip) ? a.live_prev[st.w + 1] : ~0ull;
         st.pp_dirty = a.live_pp ? ((a.live_pp[st.w] | a.live_pp[st.w + 1]) != 0ull) : true;
         st.s2 = *reinterpret_cast<const ulonglong2*>(a.seen + (uint64_t)st.v * a.stride + st.w);
     }
@@ -116,7 +116,8 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
             uint64_t k0 = ~0ull, k1 = ~0ull;
             if (cur.act && (cur.f0 & WF_KEEP)) k0 = a.ctl[cur.w].keep;
             if (cur.act && (cur.f1 & WF_KEEP)) k1 = a.ctl[cur.w + 1].keep;
-            const bool need = cur.act && !dead && ((cur.lp0 & ~s2.x & k0) | (cur.lp1 & ~s2.y & k1)) != 0ull;
+            const bool need = cur.act && !dead &&
+                              (a.noskip || ((cur.lp0 & ~s2.x & k0) | (cur.lp1 & ~s2.y & k1)) != 0ull);
             // Columns are allocated in 16-word tiles (one 128-B line per row, engine.hip), so the
             // read decision is made per tile: the 8 word-lanes of a tile load together and every
             // fetched line is fully used.

@@ -31,6 +31,7 @@ MODE_AUTO = 0
 MODE_CSR = 1
 F_TRACE = 1
 F_TIMING = 2
+F_NOSKIP = 4
 
 EXPORTED_SYMBOLS = (
     "gossip_last_error", "gossip_version", "gossip_seconds_to_ns", "gossip_milliseconds_to_ns",

@@ -114,6 +114,34 @@ def test_trace_parity_odd_latency(gossip, oracle):
     _trace_parity(gossip, oracle, 300, 0.02, 24, 10.37, 2.3)
 
 
+def test_work_skipping_changes_nothing(gossip):
+    # Dead-word / saturated-node skipping only removes reads that cannot add a bit: the dense
+    # pull (F_NOSKIP) must give identical counters, with collisions in play.
+    n = 6000
+    topo = gossip.Topology.gnp(n, 10.0 / (n - 1), 41, gossip.TOPO_SKIP)
+    t_cut = gossip.seconds_to_ns(8.0)
+    ev = gossip.make_schedule(n, 5, T0, t_cut, id_mask=0x3FFF)
+    a = _engine_for(gossip, topo, ev, L, t_cut).stats()
+    b = _engine_for(gossip, topo, ev, L, t_cut, flags=gossip.F_NOSKIP).stats()
+    for k in STATS:
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+
+
+def test_window_growth_is_transparent(gossip, oracle):
+    # Start with a one-tile window: the engine must widen its rows mid-run and stay exact.
+    n = 3000
+    topo = gossip.Topology.gnp(n, 8.0 / (n - 1), 42, gossip.TOPO_SKIP)
+    t_cut = gossip.seconds_to_ns(7.0)
+    ev = gossip.make_schedule(n, 6, T0, t_cut)
+    eng = _engine_for(gossip, topo, ev, L, t_cut, max_words=16)
+    st = eng.stats()
+    assert eng.counters().words_cap > 16
+    a, b = topo.links()
+    r = oracle.run_replay(n, L, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
+    for k in STATS:
+        assert np.array_equal(getattr(st, k), getattr(r, k)), k
+
+
 def test_sharded_engines_sum_to_whole(gossip):
     n = 5000
     topo = gossip.Topology.gnp(n, 12.0 / (n - 1), 31, gossip.TOPO_SKIP)
