@@ -121,6 +121,9 @@ typedef struct gossip_engine gossip_engine;
 
 #define GOSSIP_MODE_AUTO 0
 #define GOSSIP_MODE_CSR 1 /* bit-sliced frontier, CSR pull kernel              */
+#define GOSSIP_MODE_DENSE 2 /* adjacency x frontier as an int8 MFMA contraction (int32
+                               accumulate: exact per-node copy counts); dense graphs,
+                               n up to ~10^5 (the adjacency is n^2 bytes of HBM)      */
 
 typedef struct gossip_config {
     uint32_t num_nodes;
@@ -183,6 +186,9 @@ typedef struct gossip_counters {
     uint64_t pull_bytes_moved; /* bytes the pull kernels actually had to move after
                                   dead-word / saturated-node skipping (since reset)   */
     uint64_t pull_pair_edges;  /* (edge, 16-B word pair) neighbour reads (since reset) */
+    uint64_t dense_ops;        /* DENSE mode: int8 MAC ops x2 of the MFMA tiles computed
+                                  = 2 * 128 * 128 * n_pad per 128x128 output tile       */
+    uint64_t dense_tiles_skipped; /* DENSE mode: output tiles skipped as dead           */
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 int gossip_engine_reset_timing(gossip_engine* e);

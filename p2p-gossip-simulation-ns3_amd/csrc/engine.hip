@@ -116,6 +116,7 @@ __device__ __forceinline__ uint64_t group_fix(uint64_t nw, uint64_t seen, uint64
 }
 
 #include "pull_kernel.h"
+#include "dense_kernel.h"
 
 template <int LPW, int EPN>
 void launch_pull_t(uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
@@ -295,6 +296,11 @@ struct gossip_engine {
     // ---- device state
     uint64_t* d_F[2] = {nullptr, nullptr};
     uint64_t* d_seen = nullptr;
+    // DENSE mode: adjacency (int8, n_pad x n_pad) and the expanded frontier (int8, col-major)
+    bool dense = false;
+    uint32_t n_pad = 0;
+    int8_t* d_A8 = nullptr;
+    int8_t* d_F8T = nullptr;
     uint32_t *d_recv = nullptr, *d_gen = nullptr, *d_effgen = nullptr;
     uint64_t* d_sent = nullptr;
     unsigned long long* d_live[3] = {nullptr, nullptr, nullptr};  // liveness ring (tick % 3)
@@ -353,7 +359,7 @@ gossip_engine::~gossip_engine() {
     for (auto e : event_pool) hipEventDestroy(e);
     // Teardown: errors are ignored (nothing to report them to from a destructor).
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
-    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen);
+    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen); hipFree(d_A8); hipFree(d_F8T);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     for (int k = 0; k < kRing; k++) {
@@ -547,7 +553,8 @@ int gossip_engine::alloc_device() {
     const uint64_t bm = (uint64_t)n * stride * 8;
     size_t freeb = 0, totalb = 0;
     HIP_TRY(hipMemGetInfo(&freeb, &totalb));
-    const uint64_t need = 3 * bm + (uint64_t)n * 24 + (nnz * 4) + ((uint64_t)n + 1) * 8;
+    const uint64_t need = 3 * bm + (uint64_t)n * 24 + (nnz * 4) + ((uint64_t)n + 1) * 8 +
+                          (dense ? (uint64_t)stride * 64 * n_pad : 0ull);
     if (need > (uint64_t)freeb)
         return set_error(GOSSIP_ENOMEM, "device memory: need " + std::to_string(need) +
                                             " bytes for a " + std::to_string(stride) +
@@ -592,6 +599,12 @@ int gossip_engine::alloc_device() {
     }
     device_bytes = 3 * bm + (uint64_t)n * 20 + nnz * 4 + ((uint64_t)n + 1) * 8 + 2ull * stride * 8 +
                    kRing * ((uint64_t)stride * sizeof(WordCtl) + (uint64_t)bcap * sizeof(Birth) + pcap * 4);
+    if (dense) {
+        const uint64_t f8 = (uint64_t)stride * 64 * n_pad;
+        HIP_TRY(hipMalloc(&d_F8T, f8));
+        HIP_TRY(hipMemsetAsync(d_F8T, 0, f8, stream));
+        device_bytes += f8 + (uint64_t)n_pad * n_pad;
+    }
     WordCtl z{0ull, ~0ull, 0ull, 0ull, 0ull};
     ctl.assign(stride, z);
     tile_alloc.assign(stride / kTileWords, 0);
@@ -603,10 +616,6 @@ int gossip_engine::alloc_device() {
     return GOSSIP_OK;
 }
 
-// Columns are handed out in TILES of kTileWords words (1024 shares = one 128-B line per node
-// row), so every line of a frontier/seen row holds shares of the same age and the pull's
-// skip decisions are line-coherent.  Births fill the open tile word by word; an id group
-// never straddles a word.
 // Widen every node row to new_stride words (rare: the capacity estimate was short).  Rows are
 // copied with 2-D copies one bitmap at a time so the peak is 3 old + 1 new bitmaps.
 int gossip_engine::grow(uint32_t new_stride) {
@@ -656,6 +665,14 @@ int gossip_engine::grow(uint32_t new_stride) {
         if (!rc) rc = regrow_host(h_live[k], 8, stride, new_stride);
     }
     if (rc) return rc;
+    if (dense) {  // the expanded frontier is rebuilt every tick: no copy needed
+        HIP_TRY(hipFree(d_F8T));
+        d_F8T = nullptr;
+        const uint64_t f8 = (uint64_t)new_stride * 64 * n_pad;
+        HIP_TRY(hipMalloc(&d_F8T, f8));
+        HIP_TRY(hipMemset(d_F8T, 0, f8));
+        device_bytes += (uint64_t)(new_stride - stride) * 64 * n_pad;
+    }
     WordCtl z{0ull, ~0ull, 0ull, 0ull, 0ull};
     ctl.resize(new_stride, z);
     tile_alloc.resize(new_stride / kTileWords, 0);
@@ -669,6 +686,10 @@ int gossip_engine::grow(uint32_t new_stride) {
     return GOSSIP_OK;
 }
 
+// Columns are handed out in TILES of kTileWords words (1024 shares = one 128-B line per node
+// row), so every line of a frontier/seen row holds shares of the same age and the pull's
+// skip decisions are line-coherent.  Births fill the open tile word by word; an id group
+// never straddles a word.
 int gossip_engine::alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t) {
     if (open_tile >= 0 && open_bit + k > 64 && open_word_in_tile + 1 < kTileWords) {
         open_word_in_tile++;
@@ -851,12 +872,27 @@ int gossip_engine::tick_step(int64_t t) {
         const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, 2048));
         const size_t lds = a.use_lds ? (size_t)wact * 8 : 0;
         hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (dense) {  // expand the frontier to int8 (not timed as the pull)
+            dim3 eg((wact * 64u + 255u) / 256u, n_pad / 16u);
+            k_expand<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad, wact * 64u, d_F8T);
+            HIP_TRY(hipGetLastError());
+        }
         if (cfg.flags & GOSSIP_F_TIMING) {
             e0 = get_event();
             e1 = get_event();
             HIP_TRY(hipEventRecord(e0, stream));
         }
-        launch_pull(lpw, epn, grid, lds, stream, a);
+        if (dense) {
+            DenseArgs d;
+            d.A8 = d_A8; d.F8T = d_F8T; d.deg = d_deg; d.Fnext = d_F[nxt]; d.seen = d_seen;
+            d.ctl = d_ctl[slot]; d.wflags = d_wflags[slot]; d.recv = d_recv; d.sent = d_sent;
+            d.live = d_live[lv]; d.live_prev = a.live_prev; d.live_pp = a.live_pp; d.snap = snap_ptr;
+            d.acct = d_acct; d.n = n; d.n_pad = n_pad; d.stride = stride; d.wact = wact;
+            dim3 g(n_pad / 128u, wact / 2u);
+            k_dense_pull<<<g, 256, 0, stream>>>(d);
+        } else {
+            launch_pull(lpw, epn, grid, lds, stream, a);
+        }
         HIP_TRY(hipGetLastError());
         if (cfg.flags & GOSSIP_F_TIMING) {
             HIP_TRY(hipEventRecord(e1, stream));
@@ -935,7 +971,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
     if (cfg->t_cut_ns <= 0) return set_error(GOSSIP_EINVAL, "t_cut must be positive");
     if (cfg->shard_count > 1 && cfg->shard_rank >= cfg->shard_count)
         return set_error(GOSSIP_EINVAL, "shard_rank >= shard_count");
-    if (cfg->mode != GOSSIP_MODE_AUTO && cfg->mode != GOSSIP_MODE_CSR)
+    if (cfg->mode != GOSSIP_MODE_AUTO && cfg->mode != GOSSIP_MODE_CSR && cfg->mode != GOSSIP_MODE_DENSE)
         return set_error(GOSSIP_EINVAL, "unsupported mode");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
@@ -956,6 +992,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         if (e->tick_end < e->tick0) e->tick_end = e->tick0;
         e->cur = e->tick0;
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
+        e->dense = cfg->mode == GOSSIP_MODE_DENSE;
         *out = e.release();
         return GOSSIP_OK;
     } catch (const std::bad_alloc&) {
@@ -996,6 +1033,32 @@ int gossip_engine_set_graph(gossip_engine* e, uint32_t num_nodes, const int64_t*
     HIP_TRY(hipMemcpy(e->d_rowptr, row_ptr, ((size_t)e->n + 1) * 8, hipMemcpyHostToDevice));
     if (e->nnz) HIP_TRY(hipMemcpy(e->d_col, col, e->nnz * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->d_deg, e->h_peers.data(), (size_t)e->n * 4, hipMemcpyHostToDevice));
+    if (e->dense) {
+        // A[v][u] = multiplicity of u in peers(v), int8, rows/cols padded to 128 with zeros.
+        e->n_pad = (e->n + 127u) / 128u * 128u;
+        const uint64_t bytes = (uint64_t)e->n_pad * e->n_pad;
+        size_t freeb = 0, totalb = 0;
+        HIP_TRY(hipMemGetInfo(&freeb, &totalb));
+        if (bytes * 2 > (uint64_t)freeb)
+            return set_error(GOSSIP_ENOMEM, "DENSE mode: the " + std::to_string(bytes) +
+                                                "-byte adjacency does not fit; use GOSSIP_MODE_CSR");
+        HIP_TRY(hipMalloc(&e->d_A8, bytes));
+        const uint64_t rows_per = std::max<uint64_t>(1, (256ull << 20) / e->n_pad);
+        std::vector<int8_t> buf;
+        try {
+            buf.resize(rows_per * e->n_pad);
+        } catch (const std::bad_alloc&) {
+            return set_error(GOSSIP_ENOMEM, "host allocation failed");
+        }
+        for (uint64_t r0 = 0; r0 < e->n_pad; r0 += rows_per) {
+            const uint64_t r1 = std::min<uint64_t>(e->n_pad, r0 + rows_per);
+            std::fill(buf.begin(), buf.begin() + (r1 - r0) * e->n_pad, (int8_t)0);
+            for (uint64_t v = r0; v < r1 && v < e->n; v++)
+                for (int64_t j = row_ptr[v]; j < row_ptr[v + 1]; j++)
+                    buf[(v - r0) * e->n_pad + (uint32_t)col[j]] = (int8_t)(mult ? mult[j] : 1);
+            HIP_TRY(hipMemcpy(e->d_A8 + r0 * e->n_pad, buf.data(), (r1 - r0) * e->n_pad, hipMemcpyHostToDevice));
+        }
+    }
     e->have_graph = true;
     return GOSSIP_OK;
 }
@@ -1176,6 +1239,8 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     c->pull_bytes_moved = 16ull * acct[0] + 4ull * acct[1] + 16ull * (acct[2] + acct[3] + acct[4]) +
                           e->pull_launches * (8ull * (e->n + 1) + 16ull * e->n);
     c->pull_pair_edges = acct[0];
+    c->dense_ops = acct[5] * 2ull * 128ull * 128ull * e->n_pad;
+    c->dense_tiles_skipped = acct[6];
     uint64_t g = 0;
     const uint64_t done = (uint64_t)std::max<int64_t>(0, std::min(e->cur, e->tick_end) - e->tick0);
     if (!e->tick_lo.empty()) g = e->tick_lo[std::min<uint64_t>(done, e->tick_lo.size() - 1)];

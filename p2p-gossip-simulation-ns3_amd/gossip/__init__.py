@@ -29,6 +29,7 @@ TOPO_EXACT = 0
 TOPO_SKIP = 1
 MODE_AUTO = 0
 MODE_CSR = 1
+MODE_DENSE = 2
 F_TRACE = 1
 F_TIMING = 2
 F_NOSKIP = 4
@@ -71,7 +72,8 @@ class gossip_counters(C.Structure):
         ("ticks", C.c_uint64), ("pull_launches", C.c_uint64), ("pull_ms", C.c_double),
         ("pull_bytes", C.c_uint64), ("words_hw", C.c_uint32), ("words_cap", C.c_uint32),
         ("device_bytes", C.c_uint64), ("pull_bytes_moved", C.c_uint64),
-        ("pull_pair_edges", C.c_uint64),
+        ("pull_pair_edges", C.c_uint64), ("dense_ops", C.c_uint64),
+        ("dense_tiles_skipped", C.c_uint64),
     ]
 
 

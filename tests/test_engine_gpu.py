@@ -114,6 +114,26 @@ def test_trace_parity_odd_latency(gossip, oracle):
     _trace_parity(gossip, oracle, 300, 0.02, 24, 10.37, 2.3)
 
 
+@pytest.mark.parametrize("n,p,id_mask,sim", [(512, 0.3, 0, 8.0), (300, 0.05, 0xFFF, 30.0),
+                                             (1000, 0.02, 0, 12.0)])
+def test_dense_mfma_mode_matches_oracle(gossip, oracle, n, p, id_mask, sim):
+    # GOSSIP_MODE_DENSE: the same tick engine with the int8-MFMA contraction as the pull.
+    topo = gossip.Topology.gnp(n, p, 51, gossip.TOPO_EXACT)
+    t_cut = gossip.seconds_to_ns(sim - 0.1)
+    ev = gossip.make_schedule(n, 52, T0, t_cut, id_mask=id_mask)
+    eng = _engine_for(gossip, topo, ev, L, t_cut, mode=gossip.MODE_DENSE, flags=gossip.F_TRACE)
+    st = eng.stats()
+    a, b = topo.links()
+    r = oracle.run_replay(n, L, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=True)
+    for k in STATS:
+        assert np.array_equal(getattr(st, k), getattr(r, k)), k
+    node, sid, tick, hop, via = eng.trace()
+    tn, ti, tt, th, tv = r.trace
+    ek, ok = np.lexsort((sid, node)), np.lexsort((ti, tn))
+    assert np.array_equal(tick[ek], tt[ok] // L) and np.array_equal(hop[ek], th[ok])
+    assert eng.counters().dense_ops > 0
+
+
 def test_work_skipping_changes_nothing(gossip):
     # Dead-word / saturated-node skipping only removes reads that cannot add a bit: the dense
     # pull (F_NOSKIP) must give identical counters, with collisions in play.

@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Dense-graph measurements: the int8-MFMA contraction (GOSSIP_MODE_DENSE) against the
+bit-sliced CSR pull (GOSSIP_MODE_CSR) on the same dense workload.  One JSON line per run.
+
+    python tools/bench_dense.py c2            # C2: 4,096 nodes, p=0.3, full 60 s, real time
+    python tools/bench_dense.py c5 --width 512 # C5 slice: 65,536 nodes, p=0.3, one flood batch
+                                               # of `width` concurrent shares, 1 GPU
+
+MFMA utilisation = 2*M*N*K of the computed 128x128 output tiles / pull-kernel time / 5 POPS
+(the dense int8 peak: 2x the 2.5 PF dense bf16 rate, MI355X_MICROARCH.md "Matrix cores").
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "p2p-gossip-simulation-ns3_amd"))
+import gossip  # noqa: E402
+
+T0, L = 5_000_000_000, 5_000_000
+INT8_PEAK_OPS = 5.0e15
+
+
+def run(topo, ev, t_cut, mode, tick_end=None):
+    eng = gossip.Engine(topo.num_nodes, L, T0, t_cut, mode=mode, flags=gossip.F_TIMING)
+    eng.set_topology(topo)
+    eng.set_schedule(ev)
+    eng.reset_timing()
+    t0 = time.perf_counter()
+    eng.run(tick_end)
+    eng.sync()
+    wall = time.perf_counter() - t0
+    c = eng.counters()
+    st = eng.stats()
+    eng.close()
+    return wall, c, st
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("config", choices=["c2", "c5"])
+    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--nodes", type=int, default=0)
+    ap.add_argument("--modes", default="csr,dense")
+    a = ap.parse_args()
+    if a.config == "c2":
+        n = a.nodes or 4096
+        topo = gossip.Topology.gnp(n, 0.3, 2, gossip.TOPO_EXACT)
+        t_cut = gossip.seconds_to_ns(59.9)
+        ev = gossip.make_schedule(n, 2000, T0, t_cut)
+        desc = f"C2: dense G(n,p) {n} nodes p=0.3, 60 s real time ({len(ev)} shares), 1 GPU"
+    else:
+        n = a.nodes or 65536
+        t_setup = time.time()
+        topo = gossip.Topology.gnp(n, 0.3, 5, gossip.TOPO_SKIP, threads=16)
+        rng = np.random.Generator(np.random.Philox(12345))
+        origins = rng.choice(n, size=a.width, replace=False)
+        ev = gossip.events_from_arrays(np.full(a.width, T0 + 1000, np.int64), origins,
+                                       np.arange(1, a.width + 1, dtype=np.uint32))
+        t_cut = T0 + 40 * L
+        desc = (f"C5 slice: dense G(n,p) {n} nodes p=0.3, one flood batch of {a.width} concurrent "
+                f"shares at Philox-chosen origins, 1 GPU (setup {time.time() - t_setup:.0f} s)")
+    ref = None
+    for mode in a.modes.split(","):
+        m = gossip.MODE_DENSE if mode == "dense" else gossip.MODE_CSR
+        wall, c, st = run(topo, ev, t_cut, m)
+        if ref is None:
+            ref = st
+        same = all(np.array_equal(getattr(st, k), getattr(ref, k))
+                   for k in ("gen", "recv", "sent", "processed"))
+        out = {"workload": desc, "mode": mode, "wall_s": wall, "ticks": c.ticks,
+               "edge_events": c.edge_events, "edge_events_per_s": c.edge_events / wall,
+               "pull_ms_total": c.pull_ms, "pull_launches": c.pull_launches,
+               "pull_ms_avg": c.pull_ms / max(c.pull_launches, 1), "identical_to_first": same}
+        if mode == "dense":
+            out["dense_ops"] = c.dense_ops
+            out["dense_tiles_skipped"] = c.dense_tiles_skipped
+            out["mfma_tops"] = c.dense_ops / (c.pull_ms * 1e-3) / 1e12 if c.pull_ms else None
+            out["mfma_util"] = c.dense_ops / (c.pull_ms * 1e-3) / INT8_PEAK_OPS if c.pull_ms else None
+        else:
+            out["pull_bytes_moved"] = c.pull_bytes_moved
+            out["pull_tbs"] = c.pull_bytes_moved / (c.pull_ms * 1e-3) / 1e12 if c.pull_ms else None
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
