@@ -91,6 +91,7 @@ struct PullArgs {
     uint32_t wact;
     uint32_t use_lds;
     uint32_t noskip;  // diagnostic: read every peer-row word (dense pull, known byte count)
+    unsigned long long* inc;  // DENSE mode: incoming words from the MFMA GEMM (read + zeroed)
 };
 
 // Phase-ordered update of id groups inside one word (rare: only words holding groups).
@@ -301,6 +302,7 @@ struct gossip_engine {
     uint32_t n_pad = 0;
     int8_t* d_A8 = nullptr;
     int8_t* d_F8T = nullptr;
+    unsigned long long* d_inc = nullptr;  // n x stride incoming words (GEMM -> pull)
     uint32_t *d_recv = nullptr, *d_gen = nullptr, *d_effgen = nullptr;
     uint64_t* d_sent = nullptr;
     unsigned long long* d_live[3] = {nullptr, nullptr, nullptr};  // liveness ring (tick % 3)
@@ -359,7 +361,7 @@ gossip_engine::~gossip_engine() {
     for (auto e : event_pool) hipEventDestroy(e);
     // Teardown: errors are ignored (nothing to report them to from a destructor).
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
-    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen); hipFree(d_A8); hipFree(d_F8T);
+    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen); hipFree(d_A8); hipFree(d_F8T); hipFree(d_inc);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     for (int k = 0; k < kRing; k++) {
@@ -603,7 +605,9 @@ int gossip_engine::alloc_device() {
         const uint64_t f8 = (uint64_t)stride * 64 * n_pad;
         HIP_TRY(hipMalloc(&d_F8T, f8));
         HIP_TRY(hipMemsetAsync(d_F8T, 0, f8, stream));
-        device_bytes += f8 + (uint64_t)n_pad * n_pad;
+        HIP_TRY(hipMalloc(&d_inc, bm));
+        HIP_TRY(hipMemsetAsync(d_inc, 0, bm, stream));
+        device_bytes += f8 + bm + (uint64_t)n_pad * n_pad;
     }
     WordCtl z{0ull, ~0ull, 0ull, 0ull, 0ull};
     ctl.assign(stride, z);
@@ -665,13 +669,17 @@ int gossip_engine::grow(uint32_t new_stride) {
         if (!rc) rc = regrow_host(h_live[k], 8, stride, new_stride);
     }
     if (rc) return rc;
-    if (dense) {  // the expanded frontier is rebuilt every tick: no copy needed
+    if (dense) {  // expanded frontier and incoming words are rebuilt every tick: no copy
         HIP_TRY(hipFree(d_F8T));
+        HIP_TRY(hipFree(d_inc));
         d_F8T = nullptr;
+        d_inc = nullptr;
         const uint64_t f8 = (uint64_t)new_stride * 64 * n_pad;
         HIP_TRY(hipMalloc(&d_F8T, f8));
         HIP_TRY(hipMemset(d_F8T, 0, f8));
-        device_bytes += (uint64_t)(new_stride - stride) * 64 * n_pad;
+        HIP_TRY(hipMalloc(&d_inc, nb));
+        HIP_TRY(hipMemset(d_inc, 0, nb));
+        device_bytes += (uint64_t)(new_stride - stride) * (64ull * n_pad + 8ull * n);
     }
     WordCtl z{0ull, ~0ull, 0ull, 0ull, 0ull};
     ctl.resize(new_stride, z);
@@ -872,9 +880,10 @@ int gossip_engine::tick_step(int64_t t) {
         const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, 2048));
         const size_t lds = a.use_lds ? (size_t)wact * 8 : 0;
         hipEvent_t e0 = nullptr, e1 = nullptr;
+        a.inc = nullptr;
         if (dense) {  // expand the frontier to int8 (not timed as the pull)
             dim3 eg((wact * 64u + 255u) / 256u, n_pad / 16u);
-            k_expand<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad, wact * 64u, d_F8T);
+            k_expand<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad, wact * 64u, a.live_prev, d_F8T);
             HIP_TRY(hipGetLastError());
         }
         if (cfg.flags & GOSSIP_F_TIMING) {
@@ -883,21 +892,32 @@ int gossip_engine::tick_step(int64_t t) {
             HIP_TRY(hipEventRecord(e0, stream));
         }
         if (dense) {
-            DenseArgs d;
-            d.A8 = d_A8; d.F8T = d_F8T; d.deg = d_deg; d.Fnext = d_F[nxt]; d.seen = d_seen;
-            d.ctl = d_ctl[slot]; d.wflags = d_wflags[slot]; d.recv = d_recv; d.sent = d_sent;
-            d.live = d_live[lv]; d.live_prev = a.live_prev; d.live_pp = a.live_pp; d.snap = snap_ptr;
-            d.acct = d_acct; d.n = n; d.n_pad = n_pad; d.stride = stride; d.wact = wact;
-            dim3 g(n_pad / 128u, wact / 2u);
-            k_dense_pull<<<g, 256, 0, stream>>>(d);
+            // The timed kernel in DENSE mode is the MFMA contraction; its incoming words are
+            // then consumed by k_pull (dedup/state/counters, untimed).
+            GemmArgs gm;
+            gm.A8 = d_A8; gm.F8T = d_F8T; gm.inc = d_inc; gm.live_prev = a.live_prev; gm.acct = d_acct;
+            gm.n = n; gm.n_pad = n_pad; gm.stride = stride;
+            const uint32_t mb = n_pad / 128u, nt = wact / 4u, ksteps = n_pad / 128u;
+            uint32_t ks = 1;
+            while ((uint64_t)mb * nt * ks < 1024 && ks * 2 <= ksteps / 2) ks *= 2;
+            gm.ksplit = ks;
+            dim3 g(mb, nt, ks);
+            k_dense_gemm<<<g, 256, 0, stream>>>(gm);
+            HIP_TRY(hipGetLastError());
+            if (cfg.flags & GOSSIP_F_TIMING) {
+                HIP_TRY(hipEventRecord(e1, stream));
+                timers.emplace_back(e0, e1);
+            }
+            a.inc = d_inc;
+            launch_pull(lpw, 1, grid, lds, stream, a);
         } else {
             launch_pull(lpw, epn, grid, lds, stream, a);
+            if (cfg.flags & GOSSIP_F_TIMING) {
+                HIP_TRY(hipEventRecord(e1, stream));
+                timers.emplace_back(e0, e1);
+            }
         }
         HIP_TRY(hipGetLastError());
-        if (cfg.flags & GOSSIP_F_TIMING) {
-            HIP_TRY(hipEventRecord(e1, stream));
-            timers.emplace_back(e0, e1);
-        }
         pull_launches++;
         pull_bytes += 8ull * (n + 1) + 4ull * nnz + 8ull * wact * nnz + 24ull * wact * n + 16ull * n;
     }
@@ -1239,7 +1259,7 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     c->pull_bytes_moved = 16ull * acct[0] + 4ull * acct[1] + 16ull * (acct[2] + acct[3] + acct[4]) +
                           e->pull_launches * (8ull * (e->n + 1) + 16ull * e->n);
     c->pull_pair_edges = acct[0];
-    c->dense_ops = acct[5] * 2ull * 128ull * 128ull * e->n_pad;
+    c->dense_ops = acct[5];  // k_dense_gemm adds 2*M*N*K of every tile-split it computes
     c->dense_tiles_skipped = acct[6];
     uint64_t g = 0;
     const uint64_t done = (uint64_t)std::max<int64_t>(0, std::min(e->cur, e->tick_end) - e->tick0);

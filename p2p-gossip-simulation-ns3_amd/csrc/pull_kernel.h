@@ -116,8 +116,9 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
             uint64_t k0 = ~0ull, k1 = ~0ull;
             if (cur.act && (cur.f0 & WF_KEEP)) k0 = a.ctl[cur.w].keep;
             if (cur.act && (cur.f1 & WF_KEEP)) k1 = a.ctl[cur.w + 1].keep;
+            // (incoming mode must consume every live pair's incoming word: no saturation skip)
             const bool need = cur.act && !dead &&
-                              (a.noskip || ((cur.lp0 & ~s2.x & k0) | (cur.lp1 & ~s2.y & k1)) != 0ull);
+                              (a.noskip || a.inc || ((cur.lp0 & ~s2.x & k0) | (cur.lp1 & ~s2.y & k1)) != 0ull);
             // Columns are allocated in 16-word tiles (one 128-B line per row, engine.hip), so the
             // read decision is made per tile: the 8 word-lanes of a tile load together and every
             // fetched line is fully used.
@@ -131,7 +132,17 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
             for (int off = GRP / 2; off > 4; off >>= 1) gneed |= __shfl_xor(gneed, off, GRP);
             // ---- gather peer rows ----
             uint64_t acc0 = 0ull, acc1 = 0ull;
-            if (gneed) {  // uniform inside the node group
+            if (a.inc) {
+                // DENSE mode: the gather already happened as an MFMA contraction; take the
+                // incoming words and leave them zeroed for the next tick.
+                if (tneed && el == 0) {
+                    ulonglong2* ip = reinterpret_cast<ulonglong2*>(a.inc + (uint64_t)cur.v * stride + cur.w);
+                    const ulonglong2 x = *ip;
+                    acc0 = x.x;
+                    acc1 = x.y;
+                    if ((acc0 | acc1) != 0ull) *ip = make_ulonglong2(0ull, 0ull);
+                }
+            } else if (gneed) {  // uniform inside the node group
                 const uint64_t* Fw = a.Fcur + cur.w;
                 const int32_t beg = cur.beg, end = cur.end;
                 if constexpr (EPN == 1) {
