@@ -1,75 +1,98 @@
-// dense_kernel.h -- the dense-graph pull as an int8 MFMA contraction (GOSSIP_MODE_DENSE),
-// included by engine.hip after pull_kernel.h.
+// dense_kernel.h -- the dense-graph pull as an int8 MFMA contraction over bit-packed operands
+// (GOSSIP_MODE_DENSE), included by engine.hip after pull_kernel.h.
 //
-// For p ~ 0.3 the per-tick gather of GossipShareToPeers (p2pnode.cc:127-153) is what it really
-// is, an adjacency x frontier product:
-//     Inc[v][c] = sum_u A[v][u] * F[u][c]        A = multiplicity of u in peers(v) in {0,1,2}
-// run on v_mfma_i32_32x32x32_i8 with int32 accumulation, so Inc is the exact number of copies
-// of share c reaching v this tick (duplicates included).  Each adjacency byte is reused across
-// the 256 share columns of a block tile, which is why this beats streaming a frontier row per
-// edge on dense graphs.
+// For p ~ 0.3 the per-tick gather of GossipShareToPeers (p2pnode.cc:127-153) is an adjacency x
+// frontier product:
+//     Inc[v][c] = sum_u A[v][u] * F[u][c]        A[v][u] = [u in peers(v)],  F = frontier bits
+// and only Inc > 0 is needed (the pull dedups against seen).  Both operands stay bit-packed in
+// HBM -- the adjacency as n_pad x n_pad bits, the frontier transposed to one bit row per share
+// column (k_transpose) -- and are expanded to int8 in registers right before
+// v_mfma_i32_32x32x32_i8, so the GEMM streams 1/8 of the bytes an int8 adjacency would.
 //
-// Pipeline per tick: k_expand (frontier bitmap -> int8, column-major) -> k_dense_gemm (partial
-// Inc over a K range; Inc > 0 ballots OR-ed into an incoming bitmap) -> k_pull in "incoming"
-// mode (dedup, seen, counters, liveness; the same code as the sparse path).  Split-K is exact
-// because partial sums are non-negative: Inc > 0 iff some partial is > 0.
+// Expansion.  The MFMA contracts over 32 k per instruction; lane half h supplies 16 of them.  A
+// 32-bit word X holding the bits of k = 32kc .. 32kc+31 becomes the 4 dwords
+//     X & (0x01010101 << (4h + e)),  e = 0..3
+// i.e. byte b of dword e is nonzero iff bit 8b+4h+e of X is set.  A and B use the same map, so
+// the contraction is over the same k on both sides, and every product is a power of two
+// (2^(2d), or (-128)^2 for d = 7): Inc is a positive sum of at most 16384 per k, exact in int32
+// for n_pad < 131072 x 8, and Inc > 0 iff some peer u of v carries share c.  One v_and per
+// 4 bytes -- 4 VALU per fragment, 24 per 8 MFMAs -- hides under the 32-cycle MFMA issue gaps.
 //
 // Operand maps (pinned on gfx950 by tools/mfma_probe.hip with exact integer data): lane l holds
-// 16 int8 of A row (l&31) and of B column (l&31); the two lane halves (l>>5) hold the two
-// 16-wide k halves (any k order shared by A and B gives the same product); C/D: lane l,
-// register g -> row (g&3) + 8(g>>2) + 4(l>>5), column l&31.
+// 16 int8 of A row (l&31) and of B column (l&31); any k order shared by A and B gives the same
+// product; C/D: lane l, register g -> row (g&3) + 8(g>>2) + 4(l>>5), column l&31.
 //
-// Tiling: block = 4 waves (2 x 2), output tile 128 rows x 256 columns (4 frontier words), wave
-// tile 64 x 128 = 2 x 4 MFMA tiles (128 accumulator registers).  K advances 128 bytes per step
-// through LDS rows padded to 144 B (16 lanes of a ds_read_b128 group hit 16 distinct 16-B slots:
-// 9r mod 16 is a permutation).  The next step's global loads are issued before the current
-// step's MFMAs (register prefetch) so HBM/L2 latency hides under 32 MFMAs per wave.
+// Tiling: block = 8 waves (2 x 4), output tile 256 rows x 256 columns (4 frontier words), wave
+// tile 128 x 64 = 4 x 2 MFMA tiles (128 accumulator registers).  K advances 512 (64 B of bits
+// per row) per stage through double-buffered LDS (2 x 40 KB, rows padded to 80 B: 5r mod 16 is a
+// permutation, so 16 lanes' ds_read_b128 hit distinct 16-B slots).  One barrier per stage: the
+// stage's bit loads are issued a stage ahead.  A stage whose frontier bits are all zero for the
+// block's 256 columns is skipped (__syncthreads_or), so sparse frontiers cost only the loads.
+// Blocks are mapped XCD-major: the 4 column tiles of one row block run on one XCD together, so
+// the adjacency is fetched from HBM once per tick and re-read from that XCD's L2.
 #pragma once
 
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v16i_t __attribute__((ext_vector_type(16)));
 
-struct GemmArgs {
-    const int8_t* A8;   // n_pad x n_pad, row-major, multiplicities
-    const int8_t* F8T;  // ncols x n_pad, column-major frontier (F8T[c * n_pad + u])
-    unsigned long long* inc;  // n x stride incoming words (OR of Inc > 0)
-    const unsigned long long* live_prev;  // nullable
-    unsigned long long* acct;             // [5] += MAC ops x2, [6] += tiles skipped
-    uint32_t n, n_pad, stride, ksplit;
+struct BitsArgs {
+    const uint32_t* Ab;  // n_pad rows x kw words: bit (u & 31) of word (u >> 5) = [u in peers(v)]
+    const uint32_t* FT;  // ncols rows x kw words: bit u of row c = bit c of the frontier row u
+    unsigned long long* inc;              // n x stride incoming words (OR of Inc > 0)
+    const unsigned long long* live_prev;  // nullable: per-word liveness of the frontier
+    unsigned long long* acct;             // [5] += MAC ops x2 executed, [6] += tiles skipped
+    uint32_t n, n_pad, kw, stride;
+    uint32_t mb, nt, ksplit, total;  // row blocks, column tiles, K splits, mb*nt*ksplit
 };
 
-// F (bitmap rows) -> F8T (int8, column-major).  Thread = (column c, 16 consecutive u).
-__global__ __launch_bounds__(256) void k_expand(const uint64_t* __restrict__ F, uint32_t stride,
-                                                uint32_t n, uint32_t n_pad, uint32_t ncols,
-                                                const unsigned long long* live_prev,
-                                                int8_t* __restrict__ F8T) {
-    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t u0 = blockIdx.y * 16u;
-    if (c >= ncols) return;
-    const uint32_t w = c >> 6, b = c & 63u;
-    if (live_prev) {  // a 4-word GEMM column tile with no live word is skipped by the GEMM
+constexpr uint32_t kDenseTile = 256;   // rows / columns per block tile
+constexpr uint32_t kStageK = 512;      // k per LDS stage
+constexpr uint32_t kStageRow = 80;     // padded LDS row: 64 B of bits + 16
+constexpr uint32_t kDensePad = 512;    // n_pad multiple (tile and stage)
+
+// Frontier bitmap (node rows of share words) -> one bit row per share column.  A wave takes
+// 64 nodes x one word and transposes the 64 x 64 bit block with ballots.
+__global__ __launch_bounds__(256) void k_transpose(const uint64_t* __restrict__ F, uint32_t stride,
+                                                   uint32_t n, uint32_t kw, uint32_t nwords,
+                                                   const unsigned long long* live_prev,
+                                                   uint32_t* __restrict__ FT) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t chunk = blockIdx.x * 4u + (threadIdx.x >> 6);  // 64-node chunk
+    const uint32_t w = blockIdx.y;
+    if (w >= nwords || chunk * 64u >= kw * 32u) return;
+    if (live_prev) {  // a 4-word column tile with no live word is skipped by the GEMM
         const uint32_t g = w & ~3u;
         if ((live_prev[g] | live_prev[g + 1] | live_prev[g + 2] | live_prev[g + 3]) == 0ull) return;
     }
-    uint32_t out[4] = {0u, 0u, 0u, 0u};
+    const uint32_t u = chunk * 64u + lane;
+    const uint64_t x = (u < n) ? F[(uint64_t)u * stride + w] : 0ull;
+    uint64_t keep = 0ull;
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-        const uint32_t u = u0 + i;
-        const uint32_t bit = (u < n) ? (uint32_t)((F[(uint64_t)u * stride + w] >> b) & 1ull) : 0u;
-        out[i >> 2] |= bit << (8 * (i & 3));
+    for (int b = 0; b < 64; b++) {
+        const unsigned long long m = __ballot((x >> b) & 1ull);
+        if (lane == (uint32_t)b) keep = m;
     }
-    *reinterpret_cast<uint4*>(F8T + (uint64_t)c * n_pad + u0) = make_uint4(out[0], out[1], out[2], out[3]);
+    // row c = 64w + lane; this chunk's 64 node bits are words 2*chunk, 2*chunk+1 of the row
+    uint64_t* row = reinterpret_cast<uint64_t*>(FT + (uint64_t)(w * 64u + lane) * kw);
+    row[chunk] = keep;
 }
 
-constexpr int kGRow = 144;  // padded LDS row (bytes) for a 128-byte k slice
+__device__ __forceinline__ v4i_t dense_expand(uint32_t x, const uint32_t (&m)[4]) {
+    return v4i_t{(int)(x & m[0]), (int)(x & m[1]), (int)(x & m[2]), (int)(x & m[3])};
+}
 
-__global__ __launch_bounds__(256, 2) void k_dense_gemm(GemmArgs a) {
-    __shared__ __attribute__((aligned(16))) int8_t As[128 * kGRow];
-    __shared__ __attribute__((aligned(16))) int8_t Bs[256 * kGRow];
-    const uint32_t m0 = blockIdx.x * 128u;
-    const uint32_t w0 = blockIdx.y * 4u;  // four frontier words = 256 columns
+__global__ __launch_bounds__(512, 1) void k_dense_bits(BitsArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[2][2][kDenseTile * kStageRow];
+    // XCD-major tile order: hardware places block b on XCD b % 8; tile T = xcd * per + b / 8
+    const uint32_t per = (a.total + 7u) / 8u;
+    const uint32_t T = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    if (T >= a.total) return;
+    const uint32_t z = T % a.ksplit;
+    const uint32_t nt = (T / a.ksplit) % a.nt;
+    const uint32_t mblk = T / (a.ksplit * a.nt);
     const uint32_t t = threadIdx.x, lane = t & 63u, wid = t >> 6;
-    const uint32_t wm = wid >> 1, wn = wid & 1u;
+    const uint32_t wm = wid >> 2, wn = wid & 3u;
+    const uint32_t w0 = nt * 4u;
     if (a.live_prev) {
         const unsigned long long lv = a.live_prev[w0] | a.live_prev[w0 + 1] | a.live_prev[w0 + 2] |
                                       a.live_prev[w0 + 3];
@@ -78,84 +101,105 @@ __global__ __launch_bounds__(256, 2) void k_dense_gemm(GemmArgs a) {
             return;
         }
     }
-    const uint32_t ksteps = a.n_pad / 128u;
-    const uint32_t per = (ksteps + a.ksplit - 1u) / a.ksplit;
-    const uint32_t kb = blockIdx.z * per, ke = min(ksteps, kb + per);
-    if (kb >= ke) return;
+    const uint32_t nst = a.n_pad / kStageK;
+    const uint32_t sper = (nst + a.ksplit - 1u) / a.ksplit;
+    const uint32_t sb = z * sper, se = min(nst, sb + sper);
+    if (sb >= se) return;
 
-    v16i_t acc[2][4];
+    // loader: threads 0-255 stage adjacency rows, 256-511 frontier columns; 64 B each per stage
+    const uint32_t op = t >> 8, lrow = t & 255u;
+    const uint32_t* src = op == 0 ? a.Ab + (uint64_t)(mblk * kDenseTile + lrow) * a.kw
+                                  : a.FT + (uint64_t)(nt * kDenseTile + lrow) * a.kw;
+    uint4 r[4];
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+    for (int q = 0; q < 4; q++) r[q] = *reinterpret_cast<const uint4*>(src + (uint64_t)sb * 16u + 4u * q);
+
+    const uint32_t h = lane >> 5, rr = lane & 31u;
+    uint32_t msk[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) acc[i][j] = v16i_t{0};
-    const uint32_t r = lane & 31u, h = lane >> 5;
-    // tile loaders: A -- row t>>1, 64-byte half t&1 (4 x 16 B); B -- column t (8 x 16 B)
-    const int8_t* Ag = a.A8 + (uint64_t)(m0 + (t >> 1)) * a.n_pad + (t & 1u) * 64u;
-    const int8_t* Bg = a.F8T + (uint64_t)(w0 * 64u + t) * a.n_pad;
-    int8_t* Aw = As + (t >> 1) * kGRow + (t & 1u) * 64u;
-    int8_t* Bw = Bs + t * kGRow;
-    uint4 ra[4], rb[8];
-    {
-        const uint64_t k0 = (uint64_t)kb * 128u;
+    for (int e = 0; e < 4; e++) msk[e] = 0x01010101u << (4u * h + (uint32_t)e);
+    v16i_t acc[4][2];
 #pragma unroll
-        for (int q = 0; q < 4; q++) ra[q] = *reinterpret_cast<const uint4*>(Ag + k0 + 16 * q);
+    for (int i = 0; i < 4; i++)
 #pragma unroll
-        for (int q = 0; q < 8; q++) rb[q] = *reinterpret_cast<const uint4*>(Bg + k0 + 16 * q);
-    }
-    for (uint32_t ks = kb; ks < ke; ks++) {
-        __syncthreads();  // everyone finished reading the previous step's tiles
+        for (int j = 0; j < 2; j++) acc[i][j] = v16i_t{0};
+
+    uint32_t computed = 0;
+    for (uint32_t s = sb; s < se; s++) {
+        const uint32_t p = (s - sb) & 1u;
+        uint8_t* wr = &S[p][op][lrow * kStageRow];
 #pragma unroll
-        for (int q = 0; q < 4; q++) *reinterpret_cast<uint4*>(Aw + 16 * q) = ra[q];
-#pragma unroll
-        for (int q = 0; q < 8; q++) *reinterpret_cast<uint4*>(Bw + 16 * q) = rb[q];
-        __syncthreads();
-        if (ks + 1u < ke) {  // prefetch the next step while this one computes
-            const uint64_t k0 = (uint64_t)(ks + 1u) * 128u;
-#pragma unroll
-            for (int q = 0; q < 4; q++) ra[q] = *reinterpret_cast<const uint4*>(Ag + k0 + 16 * q);
-#pragma unroll
-            for (int q = 0; q < 8; q++) rb[q] = *reinterpret_cast<const uint4*>(Bg + k0 + 16 * q);
+        for (int q = 0; q < 4; q++) *reinterpret_cast<uint4*>(wr + 16 * q) = r[q];
+        int bnz = 0;
+        if (op == 1) {
+            const uint4 o = make_uint4(r[0].x | r[1].x | r[2].x | r[3].x, r[0].y | r[1].y | r[2].y | r[3].y,
+                                       r[0].z | r[1].z | r[2].z | r[3].z, r[0].w | r[1].w | r[2].w | r[3].w);
+            bnz = (o.x | o.y | o.z | o.w) != 0u;
         }
+        if (s + 1u < se) {
 #pragma unroll
-        for (uint32_t kc = 0; kc < 4; kc++) {
-            v4i_t af[2], bf[4];
+            for (int q = 0; q < 4; q++)
+                r[q] = *reinterpret_cast<const uint4*>(src + (uint64_t)(s + 1u) * 16u + 4u * q);
+        }
+        if (!__syncthreads_or(bnz)) continue;  // no frontier bit in this k range: nothing to add
+        computed++;
+        const uint8_t* As = &S[p][0][0];
+        const uint8_t* Bs = &S[p][1][0];
 #pragma unroll
-            for (int i = 0; i < 2; i++)
-                af[i] = *reinterpret_cast<const v4i_t*>(As + (wm * 64u + i * 32u + r) * kGRow + kc * 32u + 16u * h);
+        for (uint32_t kq = 0; kq < 4; kq++) {  // 128 k = 16 B of each row
+            uint4 xa[4], xb[2];
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-                bf[j] = *reinterpret_cast<const v4i_t*>(Bs + (wn * 128u + j * 32u + r) * kGRow + kc * 32u + 16u * h);
+            for (int i = 0; i < 4; i++)
+                xa[i] = *reinterpret_cast<const uint4*>(As + (wm * 128u + i * 32u + rr) * kStageRow + kq * 16u);
 #pragma unroll
-            for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 2; j++)
+                xb[j] = *reinterpret_cast<const uint4*>(Bs + (wn * 64u + j * 32u + rr) * kStageRow + kq * 16u);
 #pragma unroll
-                for (int j = 0; j < 4; j++)
-                    acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i][j], 0, 0, 0);
+            for (int kc = 0; kc < 4; kc++) {
+                v4i_t af[4], bf[2];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t x = kc == 0 ? xa[i].x : kc == 1 ? xa[i].y : kc == 2 ? xa[i].z : xa[i].w;
+                    af[i] = dense_expand(x, msk);
+                }
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    const uint32_t x = kc == 0 ? xb[j].x : kc == 1 ? xb[j].y : kc == 2 ? xb[j].z : xb[j].w;
+                    bf[j] = dense_expand(x, msk);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++)
+                        acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i][j], 0, 0, 0);
+            }
         }
     }
-    // ---- epilogue: Inc > 0 -> two 64-bit words per row (wave ballots), OR into inc ----
-    uint64_t inc0 = 0ull, inc1 = 0ull;
+    if (t == 0 && a.acct && computed)
+        atomicAdd(&a.acct[5], 2ull * kDenseTile * kDenseTile * kStageK * computed);
+    if (computed == 0) return;
+    // ---- epilogue: Inc > 0 -> one 64-bit word per row (wave ballots), OR into inc ----
+    // lane l collects rows l (lo) and l + 64 (hi) of the wave's 128
+    uint64_t lo = 0ull, hi = 0ull;
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < 4; i++)
 #pragma unroll
         for (int g = 0; g < 16; g++) {
             const unsigned long long q0 = __ballot(acc[i][0][g] > 0);
             const unsigned long long q1 = __ballot(acc[i][1][g] > 0);
-            const unsigned long long q2 = __ballot(acc[i][2][g] > 0);
-            const unsigned long long q3 = __ballot(acc[i][3][g] > 0);
-            const uint32_t rowA = (uint32_t)i * 32u + (g & 3) + 8u * (g >> 2);  // lane half 0
-            if (lane == rowA) {
-                inc0 = (q0 & 0xffffffffull) | (q1 << 32);
-                inc1 = (q2 & 0xffffffffull) | (q3 << 32);
-            }
-            if (lane == rowA + 4u) {  // lane half 1 rows sit 4 below
-                inc0 = (q0 >> 32) | (q1 & 0xffffffff00000000ull);
-                inc1 = (q2 >> 32) | (q3 & 0xffffffff00000000ull);
+            const uint64_t h0 = (q0 & 0xffffffffull) | (q1 << 32);               // lane half 0 row
+            const uint64_t h1 = (q0 >> 32) | (q1 & 0xffffffff00000000ull);       // 4 rows below
+            const uint32_t row = (uint32_t)(i & 1) * 32u + (g & 3) + 8u * (g >> 2);
+            if (i < 2) {
+                if (lane == row) lo = h0;
+                if (lane == row + 4u) lo = h1;
+            } else {
+                if (lane == row) hi = h0;
+                if (lane == row + 4u) hi = h1;
             }
         }
-    if (t == 0 && a.acct) atomicAdd(&a.acct[5], 2ull * 128ull * 256ull * 128ull * (ke - kb));
-    const uint64_t v = m0 + wm * 64u + lane;
-    if (v >= a.n) return;
-    unsigned long long* ip = a.inc + v * a.stride + w0 + wn * 2u;
-    if (inc0) atomicOr(ip, (unsigned long long)inc0);
-    if (inc1) atomicOr(ip + 1, (unsigned long long)inc1);
+    const uint64_t v = (uint64_t)mblk * kDenseTile + wm * 128u + lane;
+    unsigned long long* ip = a.inc + v * a.stride + w0 + wn;
+    if (lo && v < a.n) atomicOr(ip, (unsigned long long)lo);
+    if (hi && v + 64u < a.n) atomicOr(ip + 64ull * a.stride, (unsigned long long)hi);
 }

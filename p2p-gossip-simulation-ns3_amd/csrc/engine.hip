@@ -297,11 +297,12 @@ struct gossip_engine {
     // ---- device state
     uint64_t* d_F[2] = {nullptr, nullptr};
     uint64_t* d_seen = nullptr;
-    // DENSE mode: adjacency (int8, n_pad x n_pad) and the expanded frontier (int8, col-major)
+    // DENSE mode: adjacency bits (n_pad x n_pad) and the frontier transposed to share-column
+    // bit rows (stride*64 x n_pad bits), both uint32 words along the node index
     bool dense = false;
     uint32_t n_pad = 0;
-    int8_t* d_A8 = nullptr;
-    int8_t* d_F8T = nullptr;
+    uint32_t* d_Ab = nullptr;
+    uint32_t* d_FT = nullptr;
     unsigned long long* d_inc = nullptr;  // n x stride incoming words (GEMM -> pull)
     uint32_t *d_recv = nullptr, *d_gen = nullptr, *d_effgen = nullptr;
     uint64_t* d_sent = nullptr;
@@ -361,7 +362,7 @@ gossip_engine::~gossip_engine() {
     for (auto e : event_pool) hipEventDestroy(e);
     // Teardown: errors are ignored (nothing to report them to from a destructor).
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
-    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen); hipFree(d_A8); hipFree(d_F8T); hipFree(d_inc);
+    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     for (int k = 0; k < kRing; k++) {
@@ -556,7 +557,7 @@ int gossip_engine::alloc_device() {
     size_t freeb = 0, totalb = 0;
     HIP_TRY(hipMemGetInfo(&freeb, &totalb));
     const uint64_t need = 3 * bm + (uint64_t)n * 24 + (nnz * 4) + ((uint64_t)n + 1) * 8 +
-                          (dense ? (uint64_t)stride * 64 * n_pad : 0ull);
+                          (dense ? (uint64_t)stride * 8 * n_pad : 0ull);
     if (need > (uint64_t)freeb)
         return set_error(GOSSIP_ENOMEM, "device memory: need " + std::to_string(need) +
                                             " bytes for a " + std::to_string(stride) +
@@ -602,12 +603,12 @@ int gossip_engine::alloc_device() {
     device_bytes = 3 * bm + (uint64_t)n * 20 + nnz * 4 + ((uint64_t)n + 1) * 8 + 2ull * stride * 8 +
                    kRing * ((uint64_t)stride * sizeof(WordCtl) + (uint64_t)bcap * sizeof(Birth) + pcap * 4);
     if (dense) {
-        const uint64_t f8 = (uint64_t)stride * 64 * n_pad;
-        HIP_TRY(hipMalloc(&d_F8T, f8));
-        HIP_TRY(hipMemsetAsync(d_F8T, 0, f8, stream));
+        const uint64_t ft = (uint64_t)stride * 8 * n_pad;
+        HIP_TRY(hipMalloc(&d_FT, ft));
+        HIP_TRY(hipMemsetAsync(d_FT, 0, ft, stream));
         HIP_TRY(hipMalloc(&d_inc, bm));
         HIP_TRY(hipMemsetAsync(d_inc, 0, bm, stream));
-        device_bytes += f8 + bm + (uint64_t)n_pad * n_pad;
+        device_bytes += ft + bm + (uint64_t)n_pad * n_pad / 8;
     }
     WordCtl z{0ull, ~0ull, 0ull, 0ull, 0ull};
     ctl.assign(stride, z);
@@ -669,17 +670,17 @@ int gossip_engine::grow(uint32_t new_stride) {
         if (!rc) rc = regrow_host(h_live[k], 8, stride, new_stride);
     }
     if (rc) return rc;
-    if (dense) {  // expanded frontier and incoming words are rebuilt every tick: no copy
-        HIP_TRY(hipFree(d_F8T));
+    if (dense) {  // transposed frontier and incoming words are rebuilt every tick: no copy
+        HIP_TRY(hipFree(d_FT));
         HIP_TRY(hipFree(d_inc));
-        d_F8T = nullptr;
+        d_FT = nullptr;
         d_inc = nullptr;
-        const uint64_t f8 = (uint64_t)new_stride * 64 * n_pad;
-        HIP_TRY(hipMalloc(&d_F8T, f8));
-        HIP_TRY(hipMemset(d_F8T, 0, f8));
+        const uint64_t ft = (uint64_t)new_stride * 8 * n_pad;
+        HIP_TRY(hipMalloc(&d_FT, ft));
+        HIP_TRY(hipMemset(d_FT, 0, ft));
         HIP_TRY(hipMalloc(&d_inc, nb));
         HIP_TRY(hipMemset(d_inc, 0, nb));
-        device_bytes += (uint64_t)(new_stride - stride) * (64ull * n_pad + 8ull * n);
+        device_bytes += (uint64_t)(new_stride - stride) * (8ull * n_pad + 8ull * n);
     }
     WordCtl z{0ull, ~0ull, 0ull, 0ull, 0ull};
     ctl.resize(new_stride, z);
@@ -881,9 +882,9 @@ int gossip_engine::tick_step(int64_t t) {
         const size_t lds = a.use_lds ? (size_t)wact * 8 : 0;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         a.inc = nullptr;
-        if (dense) {  // expand the frontier to int8 (not timed as the pull)
-            dim3 eg((wact * 64u + 255u) / 256u, n_pad / 16u);
-            k_expand<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad, wact * 64u, a.live_prev, d_F8T);
+        if (dense) {  // transpose the frontier to share-column bit rows (not timed as the pull)
+            dim3 eg(n_pad / 256u, wact);
+            k_transpose<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad / 32u, wact, a.live_prev, d_FT);
             HIP_TRY(hipGetLastError());
         }
         if (cfg.flags & GOSSIP_F_TIMING) {
@@ -894,15 +895,17 @@ int gossip_engine::tick_step(int64_t t) {
         if (dense) {
             // The timed kernel in DENSE mode is the MFMA contraction; its incoming words are
             // then consumed by k_pull (dedup/state/counters, untimed).
-            GemmArgs gm;
-            gm.A8 = d_A8; gm.F8T = d_F8T; gm.inc = d_inc; gm.live_prev = a.live_prev; gm.acct = d_acct;
-            gm.n = n; gm.n_pad = n_pad; gm.stride = stride;
-            const uint32_t mb = n_pad / 128u, nt = wact / 4u, ksteps = n_pad / 128u;
-            uint32_t ks = 1;
-            while ((uint64_t)mb * nt * ks < 1024 && ks * 2 <= ksteps / 2) ks *= 2;
+            BitsArgs gm;
+            gm.Ab = d_Ab; gm.FT = d_FT; gm.inc = d_inc; gm.live_prev = a.live_prev; gm.acct = d_acct;
+            gm.n = n; gm.n_pad = n_pad; gm.kw = n_pad / 32u; gm.stride = stride;
+            gm.mb = n_pad / kDenseTile;
+            gm.nt = wact / 4u;
+            const uint32_t nst = n_pad / kStageK;
+            uint32_t ks = 1;  // split K until the chip has ~2 tiles per CU (>= 2 stages per split)
+            while ((uint64_t)gm.mb * gm.nt * ks < 512 && ks * 4 <= nst) ks *= 2;
             gm.ksplit = ks;
-            dim3 g(mb, nt, ks);
-            k_dense_gemm<<<g, 256, 0, stream>>>(gm);
+            gm.total = gm.mb * gm.nt * ks;
+            k_dense_bits<<<(gm.total + 7u) / 8u * 8u, 512, 0, stream>>>(gm);
             HIP_TRY(hipGetLastError());
             if (cfg.flags & GOSSIP_F_TIMING) {
                 HIP_TRY(hipEventRecord(e1, stream));
@@ -1054,29 +1057,39 @@ int gossip_engine_set_graph(gossip_engine* e, uint32_t num_nodes, const int64_t*
     if (e->nnz) HIP_TRY(hipMemcpy(e->d_col, col, e->nnz * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->d_deg, e->h_peers.data(), (size_t)e->n * 4, hipMemcpyHostToDevice));
     if (e->dense) {
-        // A[v][u] = multiplicity of u in peers(v), int8, rows/cols padded to 128 with zeros.
-        e->n_pad = (e->n + 127u) / 128u * 128u;
-        const uint64_t bytes = (uint64_t)e->n_pad * e->n_pad;
+        // A[v][u] = [u in peers(v)] as bits (multiplicity only scales a count the pull does not
+        // need), rows/cols padded to kDensePad with zeros.  Inc stays exact in int32 below 2^19
+        // columns (dense_kernel.h), far above any adjacency that fits in HBM as bits.
+        e->n_pad = (e->n + kDensePad - 1u) / kDensePad * kDensePad;
+        const uint64_t kw = e->n_pad / 32u;
+        const uint64_t bytes = (uint64_t)e->n_pad * kw * 4u;
         size_t freeb = 0, totalb = 0;
         HIP_TRY(hipMemGetInfo(&freeb, &totalb));
         if (bytes * 2 > (uint64_t)freeb)
             return set_error(GOSSIP_ENOMEM, "DENSE mode: the " + std::to_string(bytes) +
                                                 "-byte adjacency does not fit; use GOSSIP_MODE_CSR");
-        HIP_TRY(hipMalloc(&e->d_A8, bytes));
-        const uint64_t rows_per = std::max<uint64_t>(1, (256ull << 20) / e->n_pad);
-        std::vector<int8_t> buf;
+        HIP_TRY(hipMalloc(&e->d_Ab, bytes));
+        const uint64_t rows_per = std::max<uint64_t>(1, (256ull << 20) / (kw * 4u));
+        std::vector<uint32_t> buf;
         try {
-            buf.resize(rows_per * e->n_pad);
+            buf.resize(rows_per * kw);
         } catch (const std::bad_alloc&) {
             return set_error(GOSSIP_ENOMEM, "host allocation failed");
         }
         for (uint64_t r0 = 0; r0 < e->n_pad; r0 += rows_per) {
             const uint64_t r1 = std::min<uint64_t>(e->n_pad, r0 + rows_per);
-            std::fill(buf.begin(), buf.begin() + (r1 - r0) * e->n_pad, (int8_t)0);
-            for (uint64_t v = r0; v < r1 && v < e->n; v++)
-                for (int64_t j = row_ptr[v]; j < row_ptr[v + 1]; j++)
-                    buf[(v - r0) * e->n_pad + (uint32_t)col[j]] = (int8_t)(mult ? mult[j] : 1);
-            HIP_TRY(hipMemcpy(e->d_A8 + r0 * e->n_pad, buf.data(), (r1 - r0) * e->n_pad, hipMemcpyHostToDevice));
+            std::fill(buf.begin(), buf.begin() + (r1 - r0) * kw, 0u);
+            const uint64_t rn = std::min<uint64_t>(r1, e->n) > r0 ? std::min<uint64_t>(r1, e->n) - r0 : 0;
+            const int th = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+            gossip::parallel_for(rn, th, [&](uint64_t lo, uint64_t hi) {
+                for (uint64_t i = lo; i < hi; i++) {
+                    const uint64_t v = r0 + i;
+                    uint32_t* row = buf.data() + i * kw;
+                    for (int64_t j = row_ptr[v]; j < row_ptr[v + 1]; j++)
+                        row[(uint32_t)col[j] >> 5] |= 1u << ((uint32_t)col[j] & 31u);
+                }
+            });
+            HIP_TRY(hipMemcpy(e->d_Ab + r0 * kw, buf.data(), (r1 - r0) * kw * 4u, hipMemcpyHostToDevice));
         }
     }
     e->have_graph = true;
