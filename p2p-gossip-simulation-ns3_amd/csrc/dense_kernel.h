@@ -55,7 +55,8 @@ constexpr uint32_t kDensePad = 512;    // n_pad multiple (tile and stage)
 __global__ __launch_bounds__(256) void k_transpose(const uint64_t* __restrict__ F, uint32_t stride,
                                                    uint32_t n, uint32_t kw, uint32_t nwords,
                                                    const unsigned long long* live_prev,
-                                                   uint32_t* __restrict__ FT) {
+                                                   const unsigned long long* __restrict__ nz,
+                                                   uint32_t ntw, uint32_t* __restrict__ FT) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t chunk = blockIdx.x * 4u + (threadIdx.x >> 6);  // 64-node chunk
     const uint32_t w = blockIdx.y;
@@ -65,7 +66,9 @@ __global__ __launch_bounds__(256) void k_transpose(const uint64_t* __restrict__ 
         if ((live_prev[g] | live_prev[g + 1] | live_prev[g + 2] | live_prev[g + 3]) == 0ull) return;
     }
     const uint32_t u = chunk * 64u + lane;
-    const uint64_t x = (u < n) ? F[(uint64_t)u * stride + w] : 0ull;
+    // a tile row whose occupancy bit is clear holds stale bits: read as empty
+    const bool occ = u < n && ((nz[(uint64_t)u * ntw + (w >> 10)] >> ((w >> 4) & 63u)) & 1ull);
+    const uint64_t x = occ ? F[(uint64_t)u * stride + w] : 0ull;
     uint64_t keep = 0ull;
 #pragma unroll
     for (int b = 0; b < 64; b++) {

@@ -83,15 +83,20 @@ struct PullArgs {
     uint64_t* sent;
     unsigned long long* live;             // liveness of this tick (OR of F_next words)
     const unsigned long long* live_prev;  // liveness of tick t-1 (nullable: all live)
-    const unsigned long long* live_pp;    // liveness of tick t-2 (nullable: all dirty)
     unsigned long long* snap;             // nullable
     unsigned long long* acct;             // traffic accounting (nullable)
     uint32_t n;
     uint32_t stride;
+    uint32_t wbase;  // this launch covers words [wbase, wbase + wact) of every row
     uint32_t wact;
-    uint32_t use_lds;
     uint32_t noskip;  // diagnostic: read every peer-row word (dense pull, known byte count)
     unsigned long long* inc;  // DENSE mode: incoming words from the MFMA GEMM (read + zeroed)
+    // Tile occupancy of the frontier (CSR mode; null = legacy zero-filled F rows): bit
+    // (tile & 63) of word [u * ntw + tile / 64] says F[u]'s 16-word tile row holds a bit.
+    // Rows whose bit is clear are never read, so they are never zero-filled either.
+    const unsigned long long* nz_cur;
+    unsigned long long* nz_next;
+    uint32_t ntw;
 };
 
 // Phase-ordered update of id groups inside one word (rare: only words holding groups).
@@ -131,18 +136,13 @@ void launch_pull_e(int epn, uint32_t grid, size_t lds, hipStream_t s, const Pull
         case 2: launch_pull_t<LPW, 2>(grid, lds, s, a); break;
         case 4: launch_pull_t<LPW, 4>(grid, lds, s, a); break;
         case 8: launch_pull_t<LPW, 8>(grid, lds, s, a); break;
-        case 16: launch_pull_t<LPW, 16>(grid, lds, s, a); break;
-        case 32: launch_pull_t<LPW, 32>(grid, lds, s, a); break;
-        default: launch_pull_t<LPW, 64>(grid, lds, s, a); break;
+        default: launch_pull_t<LPW, 8>(grid, lds, s, a); break;
     }
 }
 
-// (LPW, EPN) with LPW * EPN <= 64, both powers of two.
+// (LPW, EPN) with 8 <= LPW, LPW * EPN <= 64, both powers of two.
 void launch_pull(int lpw, int epn, uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
-    switch (lpw) {
-        case 1: launch_pull_e<1>(epn, grid, lds, s, a); break;
-        case 2: launch_pull_e<2>(epn, grid, lds, s, a); break;
-        case 4: launch_pull_e<4>(epn, grid, lds, s, a); break;
+    switch (lpw) {  // lpw >= 8: one tile's 8 word-pairs sit in one lane group
         case 8: launch_pull_e<8>(epn, grid, lds, s, a); break;
         case 16: launch_pull_e<16>(epn, grid, lds, s, a); break;
         case 32: launch_pull_e<32>(epn, grid, lds, s, a); break;
@@ -165,6 +165,8 @@ struct BirthArgs {
     unsigned long long* live;
     unsigned long long* snap;  // nullable
     int64_t snap_r;            // snapshot phase threshold (valid when snap != null)
+    unsigned long long* nz;    // tile occupancy of Fnext (nullable: legacy zero-filled rows)
+    uint32_t ntw;
 };
 
 // GenerateAndGossipShare (p2pnode.cc:106-125): gen++, insert, send to all peers -- sends and
@@ -183,10 +185,16 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
     const uint64_t bit = 1ull << (x.col & 63u);
     uint64_t* fp = a.Fnext + v * a.stride + w;
     uint64_t* sp = a.seen + v * a.stride + w;
+    // Tile occupancy: a tile row the pull did not write this tick holds stale bits (it is
+    // only ever read behind its occupancy bit), so the birth writes the whole row.
+    const uint32_t tile = w >> 4;
+    unsigned long long* nzp = a.nz ? a.nz + v * a.ntw + (tile >> 6) : nullptr;
+    const unsigned long long tbit = 1ull << (tile & 63u);
+    const bool fresh = nzp && (*nzp & tbit) == 0ull;
     bool eff = true;
     if (x.kind == BIRTH_GROUP) {
         const uint64_t gm = (x.glen >= 64 ? ~0ull : ((1ull << x.glen) - 1ull)) << x.glo;
-        const uint64_t arr = *fp & gm;
+        const uint64_t arr = fresh ? 0ull : (*fp & gm);
         const uint64_t prior = (*sp & gm) & ~arr;
         if (prior) {
             eff = false;  // id already in processedShares before this tick
@@ -206,7 +214,17 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
         }
     }
     if (eff) {
-        *fp |= bit;
+        if (fresh) {
+            ulonglong2* row = reinterpret_cast<ulonglong2*>(a.Fnext + v * a.stride + (w & ~15u));
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++) {
+                const uint32_t w0 = (w & ~15u) + 2u * q;
+                row[q] = make_ulonglong2(w0 == w ? bit : 0ull, w0 + 1u == w ? bit : 0ull);
+            }
+            *nzp |= tbit;  // one birth per node per tick: no other writer of this word
+        } else {
+            *fp |= bit;
+        }
         *sp |= bit;
         a.effgen[v] += 1u;
         atomicOr(&a.live[w], (unsigned long long)bit);
@@ -297,6 +315,9 @@ struct gossip_engine {
     // ---- device state
     uint64_t* d_F[2] = {nullptr, nullptr};
     uint64_t* d_seen = nullptr;
+    // CSR mode: tile occupancy of F[0]/F[1] (n x ntw words, bit per 16-word tile row)
+    unsigned long long* d_nz[2] = {nullptr, nullptr};
+    uint32_t ntw = 0;
     // DENSE mode: adjacency bits (n_pad x n_pad) and the frontier transposed to share-column
     // bit rows (stride*64 x n_pad bits), both uint32 words along the node index
     bool dense = false;
@@ -362,7 +383,7 @@ gossip_engine::~gossip_engine() {
     for (auto e : event_pool) hipEventDestroy(e);
     // Teardown: errors are ignored (nothing to report them to from a destructor).
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
-    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
+    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     for (int k = 0; k < kRing; k++) {
@@ -568,6 +589,14 @@ int gossip_engine::alloc_device() {
     HIP_TRY(hipMemsetAsync(d_F[0], 0, bm, stream));
     HIP_TRY(hipMemsetAsync(d_F[1], 0, bm, stream));
     HIP_TRY(hipMemsetAsync(d_seen, 0, bm, stream));
+    {
+        ntw = (stride + 1023u) / 1024u;
+        const size_t nzb = (size_t)n * ntw * 8;
+        for (int k = 0; k < 2; k++) {
+            HIP_TRY(hipMalloc(&d_nz[k], nzb));
+            HIP_TRY(hipMemsetAsync(d_nz[k], 0, nzb, stream));
+        }
+    }
     HIP_TRY(hipMalloc(&d_recv, (size_t)n * 4));
     HIP_TRY(hipMalloc(&d_gen, (size_t)n * 4));
     HIP_TRY(hipMalloc(&d_effgen, (size_t)n * 4));
@@ -600,7 +629,7 @@ int gossip_engine::alloc_device() {
         HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&live_done[k], hipEventDisableTiming));
     }
-    device_bytes = 3 * bm + (uint64_t)n * 20 + nnz * 4 + ((uint64_t)n + 1) * 8 + 2ull * stride * 8 +
+    device_bytes = 3 * bm + 16ull * n * ntw + (uint64_t)n * 20 + nnz * 4 + ((uint64_t)n + 1) * 8 + 2ull * stride * 8 +
                    kRing * ((uint64_t)stride * sizeof(WordCtl) + (uint64_t)bcap * sizeof(Birth) + pcap * 4);
     if (dense) {
         const uint64_t ft = (uint64_t)stride * 8 * n_pad;
@@ -660,6 +689,22 @@ int gossip_engine::grow(uint32_t new_stride) {
         p = reinterpret_cast<std::remove_reference_t<decltype(p)>>(q);
         return GOSSIP_OK;
     };
+    const uint32_t new_ntw = (new_stride + 1023u) / 1024u;
+    if (new_ntw != ntw) {  // tile numbering is unchanged: widen the nz rows
+        for (int k = 0; k < 2; k++) {
+            unsigned long long* q = nullptr;
+            const size_t nzb = (size_t)n * new_ntw * 8;
+            HIP_TRY(hipMalloc(&q, nzb));
+            HIP_TRY(hipMemsetAsync(q, 0, nzb, stream));
+            HIP_TRY(hipMemcpy2DAsync(q, (size_t)new_ntw * 8, d_nz[k], (size_t)ntw * 8, (size_t)ntw * 8, n,
+                                     hipMemcpyDeviceToDevice, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            HIP_TRY(hipFree(d_nz[k]));
+            d_nz[k] = q;
+        }
+        device_bytes += 16ull * n * (new_ntw - ntw);
+        ntw = new_ntw;
+    }
     int rc = 0;
     for (int k = 0; k < 3 && !rc; k++) rc = regrow_dev(d_live[k], 8, stride, new_stride);
     for (int k = 0; k < kRing && !rc; k++) {
@@ -865,26 +910,37 @@ int gossip_engine::tick_step(int64_t t) {
         a.wflags = d_wflags[slot];
         a.recv = d_recv; a.sent = d_sent; a.live = d_live[lv]; a.snap = snap_ptr;
         a.live_prev = (t - 1 >= tick0) ? d_live[(t - 1) % 3] : nullptr;
-        a.live_pp = (t - 2 >= tick0) ? d_live[(t - 2) % 3] : nullptr;
         a.acct = d_acct;
-        a.n = n; a.stride = stride; a.wact = wact;
-        a.use_lds = wact <= 8192 ? 1u : 0u;
+        a.nz_cur = d_nz[fcur];
+        a.nz_next = d_nz[nxt];
+        a.ntw = ntw;
+        a.n = n; a.stride = stride; a.wbase = 0; a.wact = wact;
         a.noskip = (cfg.flags & GOSSIP_F_NOSKIP) ? 1u : 0u;
-        // Lane layout: word-lanes cover the window in one pass when possible; spare lanes of
-        // the wave split the peer list (edge-lanes) when peers are many.
-        int lpw = 1;
-        while (lpw < 64 && 2 * lpw < (int)wact) lpw *= 2;
-        int epn = 1;
-        const double avg_deg = n ? (double)nnz / n : 0.0;
-        while (lpw * epn * 2 <= 64 && epn * 8 < avg_deg) epn *= 2;
         const uint64_t chunks = ((uint64_t)n + 63) / 64;  // 64 nodes per wave step sequence
         const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, 2048));
-        const size_t lds = a.use_lds ? (size_t)wact * 8 : 0;
+        const double avg_deg = n ? (double)nnz / n : 0.0;
+        // One launch per kPullLdsWords words of the window (its per-word state lives in LDS).
+        // Lane layout: word-lanes cover the launch's words in one pass when possible (at least
+        // the 8 word-pairs of one tile); spare lanes of the wave split the peer list
+        // (edge-lanes) when peers are many -- and never in DENSE mode, which gathers nothing.
+        auto run_pull = [&](const PullArgs& base, bool split_edges) {
+            for (uint32_t wb = 0; wb < wact; wb += kPullLdsWords) {
+                PullArgs c = base;
+                c.wbase = wb;
+                c.wact = std::min(kPullLdsWords, wact - wb);
+                int lpw = 8;
+                while (lpw < 64 && 2 * lpw < (int)c.wact) lpw *= 2;
+                int epn = 1;
+                while (split_edges && lpw * epn * 2 <= 64 && epn * 8 < avg_deg) epn *= 2;
+                launch_pull(lpw, epn, grid, pull_lds_bytes(c.wact), stream, c);
+            }
+        };
         hipEvent_t e0 = nullptr, e1 = nullptr;
         a.inc = nullptr;
         if (dense) {  // transpose the frontier to share-column bit rows (not timed as the pull)
             dim3 eg(n_pad / 256u, wact);
-            k_transpose<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad / 32u, wact, a.live_prev, d_FT);
+            k_transpose<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad / 32u, wact, a.live_prev,
+                                                d_nz[fcur], ntw, d_FT);
             HIP_TRY(hipGetLastError());
         }
         if (cfg.flags & GOSSIP_F_TIMING) {
@@ -912,9 +968,9 @@ int gossip_engine::tick_step(int64_t t) {
                 timers.emplace_back(e0, e1);
             }
             a.inc = d_inc;
-            launch_pull(lpw, 1, grid, lds, stream, a);
+            run_pull(a, false);
         } else {
-            launch_pull(lpw, epn, grid, lds, stream, a);
+            run_pull(a, true);
             if (cfg.flags & GOSSIP_F_TIMING) {
                 HIP_TRY(hipEventRecord(e1, stream));
                 timers.emplace_back(e0, e1);
@@ -930,6 +986,8 @@ int gossip_engine::tick_step(int64_t t) {
         b.Fnext = d_F[nxt]; b.seen = d_seen; b.stride = stride;
         b.gen = d_gen; b.recv = d_recv; b.effgen = d_effgen; b.sent = d_sent; b.deg = d_deg;
         b.live = d_live[lv]; b.snap = snap_ptr; b.snap_r = snap_idx >= 0 ? snaps[snap_idx].r : 0;
+        b.nz = d_nz[nxt];
+        b.ntw = ntw;
         k_births<<<(nb + 255) / 256, 256, 0, stream>>>(b);
         HIP_TRY(hipGetLastError());
     }
@@ -965,8 +1023,15 @@ int gossip_engine::decode_trace(int64_t t) {
     if (hw == 0) return GOSSIP_OK;
     std::vector<uint64_t> F((size_t)n * stride);
     HIP_TRY(hipMemcpy(F.data(), d_F[fcur], F.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> nz;
+    if (d_nz[fcur]) {
+        nz.resize((size_t)n * ntw);
+        HIP_TRY(hipMemcpy(nz.data(), d_nz[fcur], nz.size() * 8, hipMemcpyDeviceToHost));
+    }
     for (uint32_t v = 0; v < n; v++)
         for (uint32_t w = 0; w < hw; w++) {
+            const uint32_t tl = w >> 4;
+            if (!nz.empty() && !((nz[(size_t)v * ntw + (tl >> 6)] >> (tl & 63u)) & 1ull)) continue;  // stale row
             uint64_t x = F[(size_t)v * stride + w];
             while (x) {
                 const int b = __builtin_ctzll(x);
@@ -1270,7 +1335,7 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     // col indices of the node passes that pulled (4 B), own-row seen reads/writes and F_next
     // writes (16 B each), row_ptr and the per-node counters.
     c->pull_bytes_moved = 16ull * acct[0] + 4ull * acct[1] + 16ull * (acct[2] + acct[3] + acct[4]) +
-                          e->pull_launches * (8ull * (e->n + 1) + 16ull * e->n);
+                          8ull * acct[7] + e->pull_launches * (8ull * (e->n + 1) + 16ull * e->n + 8ull * e->n * e->ntw);
     c->pull_pair_edges = acct[0];
     c->dense_ops = acct[5];  // k_dense_gemm adds 2*M*N*K of every tile-split it computes
     c->dense_tiles_skipped = acct[6];

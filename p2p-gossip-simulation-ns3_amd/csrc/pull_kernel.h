@@ -10,19 +10,26 @@
 // [2wl, 2wl+1] of every 2*LPW-word pass; edge-lane el takes every EPN-th peer.  Wide windows
 // (sparse graphs) use EPN = 1, LPW = 64: a wave reads 1 KiB of one peer row per instruction.
 // Narrow windows on dense graphs use EPN > 1: lanes split the peer list, then OR-reduce.
+// A launch covers the words [wbase, wbase + wact) of every row (wact <= kPullLdsWords).
 //
-// Latency structure.  The pull is a dependent-load chain per node (row_ptr -> peer ids / own
-// seen row -> peer rows), so the kernel pipelines it: a wave owns 64 consecutive nodes and
-// loads their row_ptr once; work items (node, pass) are processed in order and the per-item
-// "stage A" loads (word flags, last two ticks' liveness, own seen pair, first 64 peer ids) of
-// item k+1 are issued before the peer-row gathers of item k, so they ride in the same round
-// trip.  Peer rows are gathered 8 at a time (8 x 16 B per lane in flight).
+// Per-word state shared by all nodes (last tick's liveness, the word flags) is staged in LDS
+// once per block, so a work item carries only its own seen pair between pipeline stages.
+//
+// Latency structure.  The pull is a dependent-load chain per node (row_ptr -> peer ids ->
+// peer occupancy words -> peer rows), so the kernel pipelines it: a wave owns 64 consecutive
+// nodes and loads their row_ptr once; work items (node, pass) run in order, and in iteration k
+// the kernel issues the own seen pair of item k+1, the peer ids of item k+2 and the peer
+// occupancy words of item k+1 before the peer-row gathers of item k, so one round trip per
+// item covers the whole chain.  Peer rows are gathered kInflight at a time (16 B per lane each).
 //
 // Work skipping (bytes the pull never moves):
 //   dead pair  -- no column of the two words had a frontier bit anywhere last tick
 //                 (live_prev == 0): nothing can arrive;
 //   saturated  -- the node has seen every live column of the pair: peer rows not read;
-//   F_next is written only where the overwritten buffer (tick t-2) may hold bits.
+//   empty row  -- a peer's 16-word tile row with no frontier bit (its occupancy bit in
+//                 nz_cur is clear) is not read: young tiles are mostly empty rows;
+//   F_next tile rows are written only when some word of the tile got a bit (and the tile's
+//   occupancy bit set); rows left unwritten hold stale bits that no reader ever loads.
 #pragma once
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
@@ -30,53 +37,33 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
     return x;
 }
 
+// Lanes of the wave for which c holds (a wave-uniform value: traffic accounting in SGPRs).
+__device__ __forceinline__ uint32_t wave_count(bool c) { return (uint32_t)__popcll(__ballot(c)); }
+
 enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u };
 
-struct PullStage {
-    uint32_t v;
-    int32_t beg, end;  // nnz < 2^31 (checked in gossip_engine_set_graph)
-    uint32_t w, pass;
-    uint32_t f0, f1;
-    uint64_t lp0, lp1;
-    ulonglong2 s2;
-    uint32_t cid;
-    bool act, pp_dirty;
-};
+constexpr uint32_t kPullLdsWords = 2048;  // words per launch: LDS liveness, new liveness, flags
+#ifndef PULL_INFLIGHT
+#define PULL_INFLIGHT 8
+#endif
+constexpr int kInflight = PULL_INFLIGHT;  // peer-row loads in flight per lane
 
+__host__ __device__ constexpr size_t pull_lds_bytes(uint32_t wact) {
+    return (size_t)wact * 16u + (((size_t)wact + 15u) & ~(size_t)15u);
+}
+
+// Peer ids of the first GRP peers of item k's node (0xffffffff past the list).
 template <int LPW, int EPN>
-__device__ __forceinline__ void pull_stage_load(const PullArgs& a, PullStage& st, uint32_t k,
-                                                uint32_t npass, uint64_t c0, int64_t rp,
-                                                int64_t rp_end, uint32_t gl, uint32_t wl,
-                                                uint32_t slot) {
-    constexpr int GRP = LPW * EPN;
-    constexpr int NPW = 64 / GRP;
-    const uint32_t step = k / npass, p = k - step * npass;
+__device__ __forceinline__ uint32_t pull_cid_load(const PullArgs& a, uint32_t step, uint64_t c0,
+                                                  int64_t rp, int64_t rp_end, uint32_t gl,
+                                                  uint32_t slot) {
+    constexpr int NPW = 64 / (LPW * EPN);
     const uint32_t idx = step * NPW + slot;
-    st.v = (uint32_t)(c0 + idx);
-    st.beg = __shfl((int)rp, (int)idx, 64);
+    const int32_t beg = __shfl((int)rp, (int)idx, 64);
     const int32_t nx = __shfl((int)rp, (int)((idx + 1u) & 63u), 64);
-    st.end = (idx + 1u < 64u) ? nx : (int32_t)rp_end;
-    st.pass = p;
-    st.w = p * 2u * LPW + 2u * wl;
-    st.act = c0 + idx < a.n && st.w < a.wact;
-    st.f0 = st.f1 = 0;
-    st.lp0 = st.lp1 = 0ull;
-    st.pp_dirty = false;
-    st.s2 = make_ulonglong2(0ull, 0ull);
-    st.cid = 0u;
-    if (st.act) {
-        const uint16_t fl = *reinterpret_cast<const uint16_t*>(a.wflags + st.w);
-        st.f0 = fl & 0xffu;
-        st.f1 = fl >> 8;
-        st.lp0 = (a.live_prev && !a.noskip) ? a.live_prev[st.w] : ~0ull;
-        st.lp1 = (a.live_prev && !a.noskip) ? a.live_prev[st.w + 1] : ~0ull;
-        st.pp_dirty = a.live_pp ? ((a.live_pp[st.w] | a.live_pp[st.w + 1]) != 0ull) : true;
-        st.s2 = *reinterpret_cast<const ulonglong2*>(a.seen + (uint64_t)st.v * a.stride + st.w);
-    }
-    if constexpr (EPN == 1) {
-        const int32_t jj = st.beg + (int32_t)gl;
-        if (c0 + idx < a.n && jj < st.end) st.cid = (uint32_t)a.col[jj];
-    }
+    const int32_t end = (idx + 1u < 64u) ? nx : (int32_t)rp_end;
+    const int32_t jj = beg + (int32_t)gl;
+    return (c0 + idx < a.n && jj < end) ? (uint32_t)a.col[jj] : 0xffffffffu;
 }
 
 template <int LPW, int EPN>
@@ -84,11 +71,16 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
     constexpr int GRP = LPW * EPN;  // lanes per node
     constexpr int NPW = 64 / GRP;   // nodes per wave step
     static_assert(GRP <= 64 && (64 % GRP) == 0, "lane layout");
-    extern __shared__ unsigned long long s_live[];
-    if (a.use_lds) {
-        for (uint32_t i = threadIdx.x; i < a.wact; i += 256) s_live[i] = 0ull;
-        __syncthreads();
+    extern __shared__ unsigned long long smem[];
+    unsigned long long* s_lp = smem;             // live_prev of this launch's words
+    unsigned long long* s_new = smem + a.wact;   // liveness of this tick (OR of new bits)
+    uint8_t* s_wf = reinterpret_cast<uint8_t*>(smem + 2u * a.wact);
+    for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
+        s_lp[i] = (a.live_prev && !a.noskip) ? a.live_prev[a.wbase + i] : ~0ull;
+        s_new[i] = 0ull;
+        s_wf[i] = a.wflags[a.wbase + i];
     }
+    __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane % GRP, wl = gl % LPW, el = gl / LPW, slot = lane / GRP;
     const uint64_t stride = a.stride;
@@ -96,29 +88,86 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
     const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint32_t npass = (a.wact + 2u * LPW - 1u) / (2u * LPW);
-    const uint32_t nitems = (64u / NPW) * npass;
+    const uint32_t nsteps = 64u / NPW;
     unsigned long long snap_local = 0ull;
-    unsigned long long t_pe = 0, t_col = 0, t_srd = 0, t_swr = 0, t_fwr = 0;
+    uint32_t t_pe = 0, t_col = 0, t_srd = 0, t_swr = 0, t_fwr = 0, t_nz = 0;  // wave-uniform
+    unsigned long long nzacc = 0ull;
+    const bool gather = a.inc == nullptr && EPN == 1;  // the pipelined id/occupancy loads
 
     for (uint64_t c0 = wave * 64u; c0 < n; c0 += nwaves * 64u) {
         const int64_t rp = a.rowptr[min(c0 + lane, n)];
         const int64_t rp_end = a.rowptr[min(c0 + 64u, n)];
-        PullStage cur, nxt;
-        pull_stage_load<LPW, EPN>(a, cur, 0u, npass, c0, rp, rp_end, gl, wl, slot);
+        // item k = (step, pass): node c0 + step * NPW + slot, words wbase + pass * 2 LPW + 2 wl
+        uint32_t step = 0, pass = 0;
+        ulonglong2 s2c = make_ulonglong2(0ull, 0ull);
+        {
+            const uint64_t v = c0 + slot;
+            const uint32_t w = a.wbase + 2u * wl;
+            if (v < n && w < a.wbase + a.wact) s2c = *reinterpret_cast<const ulonglong2*>(a.seen + v * stride + w);
+        }
+        uint32_t cid0 = 0xffffffffu, cid1 = 0xffffffffu;
+        unsigned long long nz0 = 0ull;
+        if (gather) {
+            cid0 = pull_cid_load<LPW, EPN>(a, 0u, c0, rp, rp_end, gl, slot);
+            cid1 = npass > 1u ? cid0 : pull_cid_load<LPW, EPN>(a, 1u, c0, rp, rp_end, gl, slot);
+            nz0 = cid0 != 0xffffffffu ? a.nz_cur[(uint64_t)cid0 * a.ntw + (a.wbase >> 10)] : 0ull;
+            t_nz += wave_count(cid0 != 0xffffffffu);
+        }
         uint32_t cnt = 0;
-        for (uint32_t k = 0; k < nitems; k++) {
-            if (k + 1u < nitems) pull_stage_load<LPW, EPN>(a, nxt, k + 1u, npass, c0, rp, rp_end, gl, wl, slot);
+        while (step < nsteps) {
+            // ---- geometry of this item and the next two ----
+            const uint32_t step1 = pass + 1u < npass ? step : step + 1u;
+            const uint32_t pass1 = pass + 1u < npass ? pass + 1u : 0u;
+            const uint32_t step2 = pass1 + 1u < npass ? step1 : step1 + 1u;
+            const uint32_t idx = step * NPW + slot;
+            const uint32_t v = (uint32_t)(c0 + idx);
+            const uint32_t w = a.wbase + pass * 2u * LPW + 2u * wl;
+            const bool act = c0 + idx < n && w < a.wbase + a.wact;
+            // ---- stage loads: own seen pair of item k+1, ids of k+2, occupancy of k+1 ----
+            ulonglong2 s2n = make_ulonglong2(0ull, 0ull);
+            if (step1 < nsteps) {
+                const uint64_t v1 = c0 + step1 * NPW + slot;
+                const uint32_t w1 = a.wbase + pass1 * 2u * LPW + 2u * wl;
+                if (v1 < n && w1 < a.wbase + a.wact)
+                    s2n = *reinterpret_cast<const ulonglong2*>(a.seen + v1 * stride + w1);
+            }
+            uint32_t cid2 = 0xffffffffu;
+            unsigned long long nz1 = 0ull;
+            if (gather) {
+                if (step2 < nsteps)
+                    cid2 = step2 == step1 ? cid1 : pull_cid_load<LPW, EPN>(a, step2, c0, rp, rp_end, gl, slot);
+                if (step1 < nsteps) {
+                    const uint32_t tw1 = (a.wbase + pass1 * 2u * LPW) >> 10;
+                    const uint32_t tw0 = (a.wbase + pass * 2u * LPW) >> 10;
+                    if (step1 == step && tw1 == tw0) {
+                        nz1 = nz0;  // same node, same occupancy word
+                    } else {
+                        nz1 = cid1 != 0xffffffffu ? a.nz_cur[(uint64_t)cid1 * a.ntw + tw1] : 0ull;
+                        t_nz += wave_count(cid1 != 0xffffffffu);
+                    }
+                }
+            }
             // ---- decide: is any peer row worth reading for this pair? ----
-            const bool dead = (cur.lp0 | cur.lp1) == 0ull;
-            ulonglong2 s2 = cur.s2;
-            if (cur.f0 & WF_CLEAR) s2.x = 0ull;
-            if (cur.f1 & WF_CLEAR) s2.y = 0ull;
+            uint32_t f0 = 0, f1 = 0;
+            uint64_t lp0 = 0ull, lp1 = 0ull;
+            if (act) {
+                const uint32_t lw = w - a.wbase;
+                const uint16_t fl = *reinterpret_cast<const uint16_t*>(s_wf + lw);
+                f0 = fl & 0xffu;
+                f1 = fl >> 8;
+                lp0 = s_lp[lw];
+                lp1 = s_lp[lw + 1u];
+            }
+            const bool dead = (lp0 | lp1) == 0ull;
+            ulonglong2 s2 = s2c;
+            if (f0 & WF_CLEAR) s2.x = 0ull;
+            if (f1 & WF_CLEAR) s2.y = 0ull;
             uint64_t k0 = ~0ull, k1 = ~0ull;
-            if (cur.act && (cur.f0 & WF_KEEP)) k0 = a.ctl[cur.w].keep;
-            if (cur.act && (cur.f1 & WF_KEEP)) k1 = a.ctl[cur.w + 1].keep;
+            if (act && (f0 & WF_KEEP)) k0 = a.ctl[w].keep;
+            if (act && (f1 & WF_KEEP)) k1 = a.ctl[w + 1].keep;
             // (incoming mode must consume every live pair's incoming word: no saturation skip)
-            const bool need = cur.act && !dead &&
-                              (a.noskip || a.inc || ((cur.lp0 & ~s2.x & k0) | (cur.lp1 & ~s2.y & k1)) != 0ull);
+            const bool need = act && !dead &&
+                              (a.noskip || a.inc || ((lp0 & ~s2.x & k0) | (lp1 & ~s2.y & k1)) != 0ull);
             // Columns are allocated in 16-word tiles (one 128-B line per row, engine.hip), so the
             // read decision is made per tile: the 8 word-lanes of a tile load together and every
             // fetched line is fully used.
@@ -126,74 +175,104 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
             tn |= __shfl_xor(tn, 1, GRP);
             tn |= __shfl_xor(tn, 2, GRP);
             tn |= __shfl_xor(tn, 4, GRP);
-            const bool tneed = tn != 0 && cur.act;
+            const bool tneed = tn != 0 && act;
             int gneed = tn;
 #pragma unroll
             for (int off = GRP / 2; off > 4; off >>= 1) gneed |= __shfl_xor(gneed, off, GRP);
             // ---- gather peer rows ----
+            const uint32_t tw = w >> 10;  // one occupancy word per pass: a pass spans <= 8 tiles of 64
+            const unsigned long long tbit = 1ull << ((w >> 4) & 63u);
+            const int32_t beg = __shfl((int)rp, (int)idx, 64);
+            const int32_t nxb = __shfl((int)rp, (int)((idx + 1u) & 63u), 64);
+            const int32_t end = (idx + 1u < 64u) ? nxb : (int32_t)rp_end;
             uint64_t acc0 = 0ull, acc1 = 0ull;
             if (a.inc) {
                 // DENSE mode: the gather already happened as an MFMA contraction; take the
                 // incoming words and leave them zeroed for the next tick.
                 if (tneed && el == 0) {
-                    ulonglong2* ip = reinterpret_cast<ulonglong2*>(a.inc + (uint64_t)cur.v * stride + cur.w);
+                    ulonglong2* ip = reinterpret_cast<ulonglong2*>(a.inc + (uint64_t)v * stride + w);
                     const ulonglong2 x = *ip;
                     acc0 = x.x;
                     acc1 = x.y;
                     if ((acc0 | acc1) != 0ull) *ip = make_ulonglong2(0ull, 0ull);
                 }
             } else if (gneed) {  // uniform inside the node group
-                const uint64_t* Fw = a.Fcur + cur.w;
-                const int32_t beg = cur.beg, end = cur.end;
+                const uint64_t* Fw = a.Fcur + w;
                 if constexpr (EPN == 1) {
                     for (int32_t cb = beg; cb < end; cb += GRP) {
-                        uint32_t cid = cur.cid;
-                        if (cb != beg) {
+                        uint32_t cid = cid0;
+                        unsigned long long nzw = nz0;
+                        const int rem = min(GRP, end - cb);
+                        if (cb != beg) {  // peers beyond the first GRP: loaded inline (rare)
                             const int32_t jj = cb + (int32_t)gl;
                             cid = (jj < end) ? (uint32_t)a.col[jj] : 0u;
+                            nzw = ((int)gl < rem) ? a.nz_cur[(uint64_t)cid * a.ntw + tw] : 0ull;
+                            t_nz += wave_count((int)gl < rem);
                         }
-                        const int rem = min(GRP, end - cb);
-                        for (int t0 = 0; t0 < rem; t0 += 8) {
-                            uint32_t u[8];
+                        t_col += wave_count((int)gl < rem);
+                        // the <= 8 occupancy bits of this pass's tiles, tested per lane by tile
+                        const uint32_t nzp = (uint32_t)(nzw >> ((((w - 2u * wl) >> 4)) & 63u)) & 0xffu;
+                        for (int t0 = 0; t0 < rem; t0 += kInflight) {
+                            uint32_t u[kInflight], z[kInflight];
 #pragma unroll
-                            for (int t = 0; t < 8; t++) u[t] = (uint32_t)__shfl((int)cid, (t0 + t) & (GRP - 1), GRP);
-                            ulonglong2 q[8];
+                            for (int t = 0; t < kInflight; t++) {
+                                u[t] = (uint32_t)__shfl((int)cid, (t0 + t) & (GRP - 1), GRP);
+                                z[t] = (uint32_t)__shfl((int)nzp, (t0 + t) & (GRP - 1), GRP);
+                            }
+                            ulonglong2 q[kInflight];
+                            uint32_t hits = 0u;
 #pragma unroll
-                            for (int t = 0; t < 8; t++) {
+                            for (int t = 0; t < kInflight; t++) {
                                 q[t] = make_ulonglong2(0ull, 0ull);
-                                if (tneed && t0 + t < rem)
-                                    q[t] = *reinterpret_cast<const ulonglong2*>(Fw + (uint64_t)u[t] * stride);
+                                const bool hit = ((z[t] >> (wl >> 3)) & 1u) != 0u;
+                                hits |= hit ? (1u << t) : 0u;
+                                const bool issue = tneed && t0 + t < rem && (hit || a.noskip);
+                                if (issue) q[t] = *reinterpret_cast<const ulonglong2*>(Fw + (uint64_t)u[t] * stride);
+                                t_pe += wave_count(issue);
                             }
+                            // (consumed after all 8 loads are in flight; a row loaded without its
+                            // occupancy bit -- NOSKIP diagnostic only -- is stale and dropped)
 #pragma unroll
-                            for (int t = 0; t < 8; t++) {
-                                acc0 |= q[t].x;
-                                acc1 |= q[t].y;
+                            for (int t = 0; t < kInflight; t++) {
+                                const bool h = (hits >> t) & 1u;
+                                acc0 |= h ? q[t].x : 0ull;
+                                acc1 |= h ? q[t].y : 0ull;
                             }
                         }
-                        if (gl == 0) t_col += (unsigned long long)rem;  // one coalesced id load per group
                     }
-                    if (tneed) t_pe += (unsigned long long)(end - beg);
                 } else {
                     // edge-lane el walks peers beg+el, beg+el+EPN, ...; 8 in flight
                     for (int32_t j0 = beg + (int32_t)el; j0 < end; j0 += 8 * EPN) {
                         uint32_t u[8];
+                        unsigned long long z[8];
 #pragma unroll
                         for (int t = 0; t < 8; t++) {
                             const int32_t j = j0 + t * EPN;
                             u[t] = (tneed && j < end) ? (uint32_t)a.col[j] : 0xffffffffu;
+                            t_col += wave_count(wl == 0 && u[t] != 0xffffffffu);
+                        }
+#pragma unroll
+                        for (int t = 0; t < 8; t++) {
+                            z[t] = 0ull;
+                            if (u[t] != 0xffffffffu) z[t] = a.nz_cur[(uint64_t)u[t] * a.ntw + tw];
+                            t_nz += wave_count(u[t] != 0xffffffffu);
                         }
                         ulonglong2 q[8];
+                        uint32_t hits = 0u;
 #pragma unroll
                         for (int t = 0; t < 8; t++) {
                             q[t] = make_ulonglong2(0ull, 0ull);
-                            if (u[t] != 0xffffffffu)
-                                q[t] = *reinterpret_cast<const ulonglong2*>(Fw + (uint64_t)u[t] * stride);
+                            const bool hit = (z[t] & tbit) != 0ull;
+                            hits |= hit ? (1u << t) : 0u;
+                            const bool issue = u[t] != 0xffffffffu && (hit || a.noskip);
+                            if (issue) q[t] = *reinterpret_cast<const ulonglong2*>(Fw + (uint64_t)u[t] * stride);
+                            t_pe += wave_count(issue);
                         }
 #pragma unroll
                         for (int t = 0; t < 8; t++) {
-                            acc0 |= q[t].x;
-                            acc1 |= q[t].y;
-                            t_col += (wl == 0 && u[t] != 0xffffffffu) ? 1u : 0u;
+                            const bool h = (hits >> t) & 1u;
+                            acc0 |= h ? q[t].x : 0ull;
+                            acc1 |= h ? q[t].y : 0ull;
                         }
                     }
                 }
@@ -204,89 +283,93 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
                     acc0 |= __shfl_xor(acc0, off, GRP);
                     acc1 |= __shfl_xor(acc1, off, GRP);
                 }
-                if (tneed && el == 0) t_pe += (unsigned long long)(cur.end - cur.beg);
             }
-            // ---- dedup, state, counters (one lane per word pair) ----
-            if (cur.act && el == 0) {
-                uint64_t* sp = a.seen + (uint64_t)cur.v * stride + cur.w;
-                uint64_t* fp = a.Fnext + (uint64_t)cur.v * stride + cur.w;
-                if (dead) {
-                    if ((cur.f0 & cur.f1) & WF_CLEAR) {
-                        *reinterpret_cast<ulonglong2*>(sp) = make_ulonglong2(0ull, 0ull);
-                        t_swr++;
-                    } else if ((cur.f0 | cur.f1) & WF_CLEAR) {
-                        sp[(cur.f0 & WF_CLEAR) ? 0 : 1] = 0ull;
-                        t_swr++;
-                    }
-                    if (cur.pp_dirty) {
-                        *reinterpret_cast<ulonglong2*>(fp) = make_ulonglong2(0ull, 0ull);
-                        t_fwr++;
-                    }
-                } else {
-                    t_srd++;
-                    uint64_t n0 = acc0 & ~s2.x & k0;
-                    uint64_t n1 = acc1 & ~s2.y & k1;
-                    if (cur.f0 & WF_GROUP) n0 = group_fix(n0, s2.x, a.ctl[cur.w].gmask, a.ctl[cur.w].gstart);
-                    if (cur.f1 & WF_GROUP) n1 = group_fix(n1, s2.y, a.ctl[cur.w + 1].gmask, a.ctl[cur.w + 1].gstart);
-                    if ((n0 | n1) != 0ull || ((cur.f0 | cur.f1) & WF_CLEAR)) {
+            // ---- dedup ----
+            uint64_t n0 = 0ull, n1 = 0ull;
+            if (act && el == 0 && !dead) {
+                n0 = acc0 & ~s2.x & k0;
+                n1 = acc1 & ~s2.y & k1;
+                if (f0 & WF_GROUP) n0 = group_fix(n0, s2.x, a.ctl[w].gmask, a.ctl[w].gstart);
+                if (f1 & WF_GROUP) n1 = group_fix(n1, s2.y, a.ctl[w + 1].gmask, a.ctl[w + 1].gstart);
+            }
+            // tile occupancy of F_next: the 8 word-lanes of a tile agree on writing the row
+            int ta = (n0 | n1) != 0ull;
+            ta |= __shfl_xor(ta, 1, GRP);
+            ta |= __shfl_xor(ta, 2, GRP);
+            ta |= __shfl_xor(ta, 4, GRP);
+            // ---- state, counters (one lane per word pair) ----
+            const bool own = act && el == 0;
+            const bool swr = own && (dead ? ((f0 | f1) & WF_CLEAR) != 0u
+                                          : ((n0 | n1) != 0ull || ((f0 | f1) & WF_CLEAR) != 0u));
+            t_fwr += wave_count(own && ta);
+            t_srd += wave_count(own && !dead);
+            t_swr += wave_count(swr);
+            if (own) {
+                uint64_t* sp = a.seen + (uint64_t)v * stride + w;
+                uint64_t* fp = a.Fnext + (uint64_t)v * stride + w;
+                if (ta) *reinterpret_cast<ulonglong2*>(fp) = make_ulonglong2(n0, n1);
+                if (swr) {
+                    if (dead && !((f0 & f1) & WF_CLEAR))
+                        sp[(f0 & WF_CLEAR) ? 0 : 1] = 0ull;
+                    else
                         *reinterpret_cast<ulonglong2*>(sp) = make_ulonglong2(s2.x | n0, s2.y | n1);
-                        t_swr++;
-                    }
-                    if ((n0 | n1) != 0ull || cur.pp_dirty) {
-                        *reinterpret_cast<ulonglong2*>(fp) = make_ulonglong2(n0, n1);
-                        t_fwr++;
-                    }
+                }
+                if (!dead) {
                     cnt += (uint32_t)(__popcll(n0) + __popcll(n1));
                     if (a.snap) {
-                        if (cur.f0 & WF_SNAP) snap_local += (unsigned long long)__popcll(n0 & a.ctl[cur.w].snap);
-                        if (cur.f1 & WF_SNAP) snap_local += (unsigned long long)__popcll(n1 & a.ctl[cur.w + 1].snap);
+                        if (f0 & WF_SNAP) snap_local += (unsigned long long)__popcll(n0 & a.ctl[w].snap);
+                        if (f1 & WF_SNAP) snap_local += (unsigned long long)__popcll(n1 & a.ctl[w + 1].snap);
                     }
-                    if (a.use_lds) {
-                        if (n0) atomicOr(&s_live[cur.w], (unsigned long long)n0);
-                        if (n1) atomicOr(&s_live[cur.w + 1], (unsigned long long)n1);
-                    } else {
-                        if (n0) atomicOr(&a.live[cur.w], (unsigned long long)n0);
-                        if (n1) atomicOr(&a.live[cur.w + 1], (unsigned long long)n1);
-                    }
+                    if (n0) atomicOr(&s_new[w - a.wbase], (unsigned long long)n0);
+                    if (n1) atomicOr(&s_new[w + 1 - a.wbase], (unsigned long long)n1);
+                }
+            }
+            // ---- occupancy word of this node, written whole once per nz word index ----
+            {
+                unsigned long long nb = (ta && own && (wl & 7u) == 0u) ? tbit : 0ull;
+#pragma unroll
+                for (int off = GRP / 2; off > 0; off >>= 1) nb |= __shfl_xor(nb, off, GRP);
+                nzacc |= nb;
+                const bool last_of_tw = pass + 1u == npass || ((a.wbase + (pass + 1u) * 2u * LPW) >> 10) != tw;
+                if (last_of_tw) {
+                    if (gl == 0 && c0 + idx < n) a.nz_next[(uint64_t)v * a.ntw + tw] = nzacc;
+                    nzacc = 0ull;
                 }
             }
             // ---- per-node counters after the node's last pass ----
-            if (cur.pass + 1u == npass) {
+            if (pass + 1u == npass) {
                 uint32_t c = cnt;
 #pragma unroll
                 for (int off = GRP / 2; off > 0; off >>= 1) c += __shfl_xor(c, off, GRP);
                 if (gl == 0 && c) {
-                    a.recv[cur.v] += c;
-                    a.sent[cur.v] += (uint64_t)c * a.deg[cur.v];
+                    a.recv[v] += c;
+                    a.sent[v] += (uint64_t)c * a.deg[v];
                 }
                 cnt = 0;
             }
-            cur = nxt;
+            // ---- advance the pipeline ----
+            s2c = s2n;
+            cid0 = cid1;
+            cid1 = cid2;
+            nz0 = nz1;
+            step = step1;
+            pass = pass1;
         }
     }
     if (a.snap) {
         snap_local = wave_sum(snap_local);
         if (lane == 0 && snap_local) atomicAdd(a.snap, snap_local);
     }
-    if (a.acct) {
-        t_pe = wave_sum(t_pe);
-        t_col = wave_sum(t_col);
-        t_srd = wave_sum(t_srd);
-        t_swr = wave_sum(t_swr);
-        t_fwr = wave_sum(t_fwr);
-        if (lane == 0) {
-            atomicAdd(&a.acct[0], t_pe);
-            atomicAdd(&a.acct[1], t_col);
-            atomicAdd(&a.acct[2], t_srd);
-            atomicAdd(&a.acct[3], t_swr);
-            atomicAdd(&a.acct[4], t_fwr);
-        }
+    if (a.acct && lane == 0) {
+        const uint32_t tv[6] = {t_pe, t_col, t_srd, t_swr, t_fwr, t_nz};
+        const int slot_of[6] = {0, 1, 2, 3, 4, 7};
+#pragma unroll
+        for (int q = 0; q < 6; q++)
+            if (tv[q]) atomicAdd(&a.acct[slot_of[q]], (unsigned long long)tv[q]);
     }
-    if (a.use_lds) {
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
-            const unsigned long long x = s_live[i];
-            if (x) atomicOr(&a.live[i], x);
-        }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
+        const unsigned long long x = s_new[i];
+        if (x) atomicOr(&a.live[a.wbase + i], x);
     }
 }

@@ -23,7 +23,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(os.path.dirname(_HERE), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libgossip.so")
+LIB_PATH = os.environ.get("GOSSIP_LIB_PATH") or os.path.join(LIB_DIR, "libgossip.so")
 
 TOPO_EXACT = 0
 TOPO_SKIP = 1
