@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=2)
     ap.add_argument("--noskip", action="store_true",
                     help="diagnostic: dense pull (every peer-row word read) for PMC calibration")
+    ap.add_argument("--pull-kernel", choices=("auto", "wide", "generic"), default="auto",
+                    help="diagnostic: force the scalar-peer (wide) or lane-shuffle (generic) pull")
     ap.add_argument("--rehearse-shards", type=int, default=0,
                     help="diagnostic: run only shard 0 of S on this one GPU (per-rank footprint "
                          "and time of an S-GPU run); the JSON line is marked REHEARSAL")
@@ -139,6 +141,7 @@ def main():
         shards = args.rehearse_shards
         wl["desc"] += f" [REHEARSAL: shard 0 of {shards} on one GPU]"
     flags = gossip.F_TIMING | (gossip.F_NOSKIP if args.noskip else 0)
+    flags |= {"auto": 0, "wide": gossip.F_WIDE_PULL, "generic": gossip.F_GENERIC_PULL}[args.pull_kernel]
     eng = gossip.Engine(n, L_NS, SLICE_NS, T_CUT_NS, device=local, flags=flags,
                         shard_rank=rank, shard_count=shards)
     eng.set_topology(topo)
@@ -188,6 +191,7 @@ def main():
         dense_bytes_per_launch = pull_bytes / max(launches, 1)  # SURVEY §8d dense formula
         achieved = bytes_per_launch / (avg_ms * 1e6) if avg_ms > 0 else 0.0  # GB/s
         traffic = pmc_traffic(wl["name"], n_gpus)
+        per_launch = lambda x: float(x) / max(launches, 1)  # noqa: E731
         out = {
             "metric": "share-deliveries/sec (edge events)",
             "value": edges_total / elapsed,
@@ -226,6 +230,18 @@ def main():
                 "dense_formula_bytes_per_launch": dense_bytes_per_launch,
                 "dense_formula_equiv_gbs": (dense_bytes_per_launch / (avg_ms * 1e6)) if avg_ms > 0 else None,
                 "avg_launch_ms": avg_ms,
+                "bytes_breakdown_per_launch": {
+                    "peer_rows": per_launch(16 * c1.pull_pair_edges),
+                    "peer_ids": per_launch(4 * c1.pull_col_ids),
+                    "peer_occupancy": per_launch(8 * c1.pull_nz_reads),
+                    "own_seen_read": per_launch(16 * c1.pull_seen_reads),
+                    "own_seen_write": per_launch(16 * c1.pull_seen_writes),
+                    "frontier_write": per_launch(16 * c1.pull_f_writes),
+                    "per_node_rowptr_counters_occupancy": per_launch(
+                        c1.pull_bytes_moved - 16 * c1.pull_pair_edges - 4 * c1.pull_col_ids -
+                        8 * c1.pull_nz_reads - 16 * (c1.pull_seen_reads + c1.pull_seen_writes +
+                                                     c1.pull_f_writes)),
+                },
                 "pull_fraction_of_step": (pull_ms_max / (elapsed * 1e3)) if elapsed > 0 else None,
             },
         }

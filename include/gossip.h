@@ -142,6 +142,10 @@ typedef struct gossip_config {
 #define GOSSIP_F_TIMING 2u /* time each pull-kernel launch with HIP events          */
 #define GOSSIP_F_NOSKIP 4u /* diagnostic: dense pull (no dead/saturated skipping);
                               results are identical, only the bytes read change       */
+#define GOSSIP_F_WIDE_PULL 8u     /* test: scalar-peer wide pull kernel at every window width */
+#define GOSSIP_F_GENERIC_PULL 16u /* diagnostic: lane-shuffle pull kernel at every width     */
+#define GOSSIP_F_TILE_PER_TICK 32u /* test: open a fresh 1024-share tile every tick (wide,
+                                      sparsely filled windows at small n)                 */
 
 int gossip_engine_create(const gossip_config* cfg, gossip_engine** out);
 /* Graph: CSR over distinct neighbours with multiplicity in {1,2} (see topology above). */
@@ -189,6 +193,12 @@ typedef struct gossip_counters {
     uint64_t dense_ops;        /* DENSE mode: int8 MAC ops x2 of the MFMA tiles computed
                                   = 2 * 128 * 128 * n_pad per 128x128 output tile       */
     uint64_t dense_tiles_skipped; /* DENSE mode: output tiles skipped as dead           */
+    /* pull traffic breakdown since reset (each a count of the unit in brackets):         */
+    uint64_t pull_col_ids;     /* peer ids loaded [4 B]                                 */
+    uint64_t pull_seen_reads;  /* own seen pairs used by live work items [16 B]         */
+    uint64_t pull_seen_writes; /* own seen pairs written [16 B]                         */
+    uint64_t pull_f_writes;    /* F_next pairs written [16 B]                           */
+    uint64_t pull_nz_reads;    /* peer tile-occupancy words loaded [8 B]                */
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 int gossip_engine_reset_timing(gossip_engine* e);

@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -745,6 +746,8 @@ int gossip_engine::grow(uint32_t new_stride) {
 // skip decisions are line-coherent.  Births fill the open tile word by word; an id group
 // never straddles a word.
 int gossip_engine::alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t) {
+    if ((cfg.flags & GOSSIP_F_TILE_PER_TICK) && open_tile >= 0 && tile_last_inject[(uint32_t)open_tile] < t)
+        open_tile = -1;
     if (open_tile >= 0 && open_bit + k > 64 && open_word_in_tile + 1 < kTileWords) {
         open_word_in_tile++;
         open_bit = 0;
@@ -932,7 +935,12 @@ int gossip_engine::tick_step(int64_t t) {
                 while (lpw < 64 && 2 * lpw < (int)c.wact) lpw *= 2;
                 int epn = 1;
                 while (split_edges && lpw * epn * 2 <= 64 && epn * 8 < avg_deg) epn *= 2;
-                launch_pull(lpw, epn, grid, pull_lds_bytes(c.wact), stream, c);
+                const bool wide = split_edges && n < (1u << 24) && !(cfg.flags & GOSSIP_F_GENERIC_PULL) &&
+                                  ((lpw == 64 && epn == 1) || (cfg.flags & GOSSIP_F_WIDE_PULL));
+                if (wide)
+                    k_pull_wide<<<grid, 256, pull_lds_bytes(c.wact), stream>>>(c);
+                else
+                    launch_pull(lpw, epn, grid, pull_lds_bytes(c.wact), stream, c);
             }
         };
         hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1339,6 +1347,11 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     c->pull_pair_edges = acct[0];
     c->dense_ops = acct[5];  // k_dense_gemm adds 2*M*N*K of every tile-split it computes
     c->dense_tiles_skipped = acct[6];
+    c->pull_col_ids = acct[1];
+    c->pull_seen_reads = acct[2];
+    c->pull_seen_writes = acct[3];
+    c->pull_f_writes = acct[4];
+    c->pull_nz_reads = acct[7];
     uint64_t g = 0;
     const uint64_t done = (uint64_t)std::max<int64_t>(0, std::min(e->cur, e->tick_end) - e->tick0);
     if (!e->tick_lo.empty()) g = e->tick_lo[std::min<uint64_t>(done, e->tick_lo.size() - 1)];

@@ -33,6 +33,9 @@ MODE_DENSE = 2
 F_TRACE = 1
 F_TIMING = 2
 F_NOSKIP = 4
+F_WIDE_PULL = 8
+F_GENERIC_PULL = 16
+F_TILE_PER_TICK = 32
 
 EXPORTED_SYMBOLS = (
     "gossip_last_error", "gossip_version", "gossip_seconds_to_ns", "gossip_milliseconds_to_ns",
@@ -73,7 +76,9 @@ class gossip_counters(C.Structure):
         ("pull_bytes", C.c_uint64), ("words_hw", C.c_uint32), ("words_cap", C.c_uint32),
         ("device_bytes", C.c_uint64), ("pull_bytes_moved", C.c_uint64),
         ("pull_pair_edges", C.c_uint64), ("dense_ops", C.c_uint64),
-        ("dense_tiles_skipped", C.c_uint64),
+        ("dense_tiles_skipped", C.c_uint64), ("pull_col_ids", C.c_uint64),
+        ("pull_seen_reads", C.c_uint64), ("pull_seen_writes", C.c_uint64),
+        ("pull_f_writes", C.c_uint64), ("pull_nz_reads", C.c_uint64),
     ]
 
 

@@ -75,13 +75,18 @@ def test_report_text_matches_oracle(gossip, oracle):
     assert sim.PrintPeriodicStats() == want
 
 
-def _trace_parity(gossip, oracle, n, p, seed, sim_time, lat_ms, kind=None, id_mask=0):
+# Pull kernels: the default choice by window width (lane-shuffle k_pull for narrow windows,
+# scalar-peer k_pull_wide above 64 words), and each kernel forced at every width.
+KERNELS = {"auto": 0, "wide": 8, "generic": 16}
+
+
+def _trace_parity(gossip, oracle, n, p, seed, sim_time, lat_ms, kind=None, id_mask=0, kflags=0):
     kind = gossip.TOPO_EXACT if kind is None else kind
     topo = gossip.Topology.gnp(n, p, seed, kind)
     lat = gossip.milliseconds_to_ns(lat_ms)
     t_cut = gossip.seconds_to_ns(sim_time - 0.1)
     ev = gossip.make_schedule(n, seed + 1, T0, t_cut, id_mask=id_mask)
-    eng = _engine_for(gossip, topo, ev, lat, t_cut, flags=gossip.F_TRACE)
+    eng = _engine_for(gossip, topo, ev, lat, t_cut, flags=gossip.F_TRACE | kflags)
     st = eng.stats()
     a, b = topo.links()
     r = oracle.run_replay(n, lat, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=True)
@@ -97,21 +102,25 @@ def _trace_parity(gossip, oracle, n, p, seed, sim_time, lat_ms, kind=None, id_ma
     assert np.array_equal(via[ek], tv[ok])
 
 
-def test_trace_parity_sparse_4096(gossip, oracle):
-    _trace_parity(gossip, oracle, 4096, 16.0 / 4095, 21, 6.0, 5.0)
+@pytest.mark.parametrize("kern", list(KERNELS))
+def test_trace_parity_sparse_4096(gossip, oracle, kern):
+    _trace_parity(gossip, oracle, 4096, 16.0 / 4095, 21, 6.0, 5.0, kflags=KERNELS[kern])
 
 
-def test_trace_parity_dense_512(gossip, oracle):
-    _trace_parity(gossip, oracle, 512, 0.3, 22, 8.0, 5.0)
+@pytest.mark.parametrize("kern", list(KERNELS))
+def test_trace_parity_dense_512(gossip, oracle, kern):
+    _trace_parity(gossip, oracle, 512, 0.3, 22, 8.0, 5.0, kflags=KERNELS[kern])
 
 
-def test_trace_parity_collisions(gossip, oracle):
+@pytest.mark.parametrize("kern", list(KERNELS))
+def test_trace_parity_collisions(gossip, oracle, kern):
     # 0x3FF id mask: dozens of generations per id, id groups of up to ~6 sources
-    _trace_parity(gossip, oracle, 400, 0.01, 23, 15.0, 5.0, id_mask=0x3FF)
+    _trace_parity(gossip, oracle, 400, 0.01, 23, 15.0, 5.0, id_mask=0x3FF, kflags=KERNELS[kern])
 
 
-def test_trace_parity_odd_latency(gossip, oracle):
-    _trace_parity(gossip, oracle, 300, 0.02, 24, 10.37, 2.3)
+@pytest.mark.parametrize("kern", list(KERNELS))
+def test_trace_parity_odd_latency(gossip, oracle, kern):
+    _trace_parity(gossip, oracle, 300, 0.02, 24, 10.37, 2.3, kflags=KERNELS[kern])
 
 
 @pytest.mark.parametrize("n,p,id_mask,sim", [(512, 0.3, 0, 8.0), (300, 0.05, 0xFFF, 30.0),
@@ -134,17 +143,35 @@ def test_dense_mfma_mode_matches_oracle(gossip, oracle, n, p, id_mask, sim):
     assert eng.counters().dense_ops > 0
 
 
-def test_work_skipping_changes_nothing(gossip):
-    # Dead-word / saturated-node skipping only removes reads that cannot add a bit: the dense
-    # pull (F_NOSKIP) must give identical counters, with collisions in play.
+@pytest.mark.parametrize("kern", list(KERNELS))
+def test_work_skipping_changes_nothing(gossip, kern):
+    # Dead-word / saturated-node / empty-row skipping only removes reads that cannot add a
+    # bit: the dense pull (F_NOSKIP) must give identical counters, with collisions in play.
     n = 6000
     topo = gossip.Topology.gnp(n, 10.0 / (n - 1), 41, gossip.TOPO_SKIP)
     t_cut = gossip.seconds_to_ns(8.0)
     ev = gossip.make_schedule(n, 5, T0, t_cut, id_mask=0x3FFF)
-    a = _engine_for(gossip, topo, ev, L, t_cut).stats()
-    b = _engine_for(gossip, topo, ev, L, t_cut, flags=gossip.F_NOSKIP).stats()
+    a = _engine_for(gossip, topo, ev, L, t_cut, flags=KERNELS[kern]).stats()
+    b = _engine_for(gossip, topo, ev, L, t_cut, flags=gossip.F_NOSKIP | KERNELS[kern]).stats()
     for k in STATS:
         assert np.array_equal(getattr(a, k), getattr(b, k)), k
+
+
+def test_wide_window_kernels_agree(gossip, oracle):
+    # A window far wider than 64 words (a fresh tile every tick): the default (k_pull_wide at
+    # this width) and the lane-shuffle kernel must match the oracle bit for bit.
+    n = 3000
+    topo = gossip.Topology.gnp(n, 6.0 / (n - 1), 43, gossip.TOPO_SKIP)
+    t_cut = gossip.seconds_to_ns(5.7)
+    ev = gossip.make_schedule(n, 7, T0, t_cut)
+    a, b = topo.links()
+    r = oracle.run_replay(n, L, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
+    for kern in KERNELS.values():
+        eng = _engine_for(gossip, topo, ev, L, t_cut, flags=kern | gossip.F_TILE_PER_TICK)
+        st = eng.stats()
+        assert eng.counters().words_hw > 64
+        for k in STATS:
+            assert np.array_equal(getattr(st, k), getattr(r, k)), (kern, k)
 
 
 def test_window_growth_is_transparent(gossip, oracle):
