@@ -1,22 +1,27 @@
 #!/usr/bin/env python3
 """Benchmark: share-deliveries/sec (edge events/s) of the MI355X gossip engine.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C4|C3]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 One step = one tick (= --Latency = 5 ms of simulated time) of the tick-synchronous engine
 over every live share column: the CSR pull over the bit-sliced frontier, dedup against the
 seen bitmap, counters, and the new generations of that tick.
 
-Workloads (BASELINE.json configs):
-  N = 1  -> C3: sparse G(n,p), 1M nodes, average degree 16, 1 GPU (the largest single-GPU
-            config; C4's full live window does not fit one GPU's HBM).
-  N > 1  -> C4: sparse G(n,p), 10M nodes, average degree 16; share columns are sharded over
-            the N ranks by share instance (no per-tick exchange, DESIGN.md "Multi-GPU"); the
-            only collectives are the barrier and the final counter all-reduce over RCCL.
-The timed window starts after W warm-up ticks from t = 5 s (the live window fills within
-~10 ticks) and covers K ticks of steady-state gossip.  Inputs are resident in HBM before
-the timed region starts.  `value` = edge events processed by all ranks / max-rank time.
+Workload (BASELINE.json metric: "share-deliveries/sec at 10M nodes, 1/2/4/8 GPUs"):
+  C4: sparse G(n,p), 10M nodes, average degree 16, every share generated in the window.
+The share columns are split into share-instance shards (gossip_shard_events; no per-tick
+exchange, DESIGN.md "Multi-GPU").  C4's live window needs two shards' worth of HBM (one shard
+holds ~265 GiB of bitmaps), so the job is always cut into max(2, N) shards: at N = 1 the one
+GPU runs shard 0 and then shard 1 (each with its own warm-up, timed separately, the times
+added); at N >= 2 every rank runs one shard.  The total work is the same at every N
+(strong scaling); the only collectives are barriers and the final scalar reductions (RCCL).
+--workload C3 (1M nodes, one shard per GPU) is kept for kernel A/B work.
+
+The timed window of a shard starts after W warm-up ticks from t = 10 s and covers K ticks of
+steady-state gossip; inputs are resident in HBM before it starts.
+`value` = edge events processed by all shards / (max over ranks of the rank's summed timed
+windows).
 
 The rank-0 N=1 run also times ORACLE A (the reference's P2PNode logic on one CPU core,
 event-driven, unordered_set seen-sets) on a bounded sample of the same workload.
@@ -40,17 +45,17 @@ SLICE_NS = 10_000_000_000  # steady-state slice start (tick 2000 at 5 ms)
 L_NS = 5_000_000
 T_CUT_NS = 59_900_000_000
 
+WORKLOADS = {
+    # fit_shards: share shards one GPU's HBM must be cut into for the live window to fit
+    "C4": dict(nodes=10_000_000, fit_shards=2, topo_seed=4, node_seed=2000,
+               desc="C4: sparse G(n,p), 10M nodes, avg degree 16, 5 ms ticks"),
+    "C3": dict(nodes=1_000_000, fit_shards=1, topo_seed=3, node_seed=1000,
+               desc="C3: sparse G(n,p), 1M nodes, avg degree 16, 5 ms ticks"),
+}
+
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
-
-
-def workload(n_gpus):
-    if n_gpus == 1:
-        return dict(name="C3", nodes=1_000_000, desc="C3: sparse G(n,p), 1M nodes, avg degree 16, "
-                    "5 ms ticks, 1 GPU", topo_seed=3, node_seed=1000)
-    return dict(name="C4", nodes=10_000_000, desc="C4: sparse G(n,p), 10M nodes, avg degree 16, "
-                "5 ms ticks, share-sharded over GPUs", topo_seed=4, node_seed=2000)
 
 
 def pmc_traffic(name, n_gpus):
@@ -66,21 +71,24 @@ def pmc_traffic(name, n_gpus):
         return None
 
 
-def cpu_baseline(topo, ev, sample_shares, threads):
-    """ORACLE A (single thread) on the first `sample_shares` generations of the workload,
-    floods run to completion.  Test infrastructure used only as the timed CPU baseline."""
+def cpu_baseline(topo, ev, sample_shares, hops):
+    """ORACLE A (single thread) on the first `sample_shares` generations of the workload's
+    steady-state slice, their floods cut after `hops` hops (PrintStatistics time).  Test
+    infrastructure used only as the timed CPU baseline."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
     a, b = topo.links()
     sub = ev[:sample_shares]
-    r = oracle.run_replay(topo.num_nodes, L_NS, SLICE_NS, oracle.INT64_MAX, a, b, sub["ns"],
-                          sub["node"], sub["share_id"])
+    t_cut = int(sub["ns"].max()) + hops * L_NS + 1 if hops > 0 else oracle.INT64_MAX
+    r = oracle.run_replay(topo.num_nodes, L_NS, SLICE_NS, t_cut, a, b, sub["ns"], sub["node"],
+                          sub["share_id"])
+    cut = f"cut after {hops} hops" if hops > 0 else "run to completion"
     return dict(value=r.edge_events / r.wall_s if r.wall_s > 0 else None, unit="edge events/s",
                 cores=1, kind="port",
                 sample=f"ORACLE A (event-driven P2PNode logic, unordered_set seen-sets) on the "
-                       f"same graph, the first {len(sub)} generations after t=10 s, floods run "
-                       f"to completion: {r.edge_events} edge events in {r.wall_s:.2f} s "
+                       f"same graph, the first {len(sub)} generation(s) after t=10 s, floods "
+                       f"{cut}: {r.edge_events} edge events in {r.wall_s:.2f} s of event loop "
                        f"(host nproc {os.cpu_count()}, threads=1)")
 
 
@@ -89,9 +97,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="C4")
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=int, default=1, help="generations in the CPU sample")
+    ap.add_argument("--cpu-hops", type=int, default=5, help="hops the CPU-sample floods run")
     ap.add_argument("--noskip", action="store_true",
                     help="diagnostic: dense pull (every peer-row word read) for PMC calibration")
     ap.add_argument("--pull-kernel", choices=("auto", "wide", "generic"), default="auto",
@@ -119,13 +129,24 @@ def main():
             dev = f"cuda:{local}"
         dist.init_process_group(backend)
         import gossip.dist as gd
-    wl = workload(n_gpus)
+    wl = dict(WORKLOADS[args.workload], name=args.workload)
     if os.environ.get("GOSSIP_BENCH_NODES"):
         wl["nodes"] = int(os.environ["GOSSIP_BENCH_NODES"])
         wl["desc"] += f" [REHEARSAL: {wl['nodes']} nodes]"
     n = wl["nodes"]
     p = 16.0 / (n - 1)
     W, K = args.warmup, args.steps
+
+    # Shards: at least what one GPU's HBM needs, at least one per rank, a multiple of the ranks.
+    passes = max(1, -(-wl["fit_shards"] // world))
+    shards = passes * world
+    my_shards = [rank * passes + q for q in range(passes)]
+    rehearsal = args.rehearse_shards > 1 and world == 1
+    if rehearsal:
+        shards, my_shards = args.rehearse_shards, [0]
+        wl["desc"] += f" [REHEARSAL: shard 0 of {shards} on one GPU]"
+    layout = (f"{shards} share shards, {len(my_shards)} per GPU in sequence" if len(my_shards) > 1
+              else f"{shards} share shards, one per GPU")
 
     t_setup = time.time()
     topo = gossip.Topology.gnp(n, p, wl["topo_seed"], gossip.TOPO_SKIP, threads=args.threads)
@@ -136,62 +157,83 @@ def main():
     ev = gossip.make_schedule(n, wl["node_seed"], T0_NS, T_CUT_NS, t_gen_end_ns=t_gen_end,
                               threads=args.threads)
     ev = ev[ev["ns"] >= SLICE_NS]
-    shards = max(world, 1)
-    if args.rehearse_shards > 1 and world == 1:
-        shards = args.rehearse_shards
-        wl["desc"] += f" [REHEARSAL: shard 0 of {shards} on one GPU]"
     flags = gossip.F_TIMING | (gossip.F_NOSKIP if args.noskip else 0)
     flags |= {"auto": 0, "wide": gossip.F_WIDE_PULL, "generic": gossip.F_GENERIC_PULL}[args.pull_kernel]
-    eng = gossip.Engine(n, L_NS, SLICE_NS, T_CUT_NS, device=local, flags=flags,
-                        shard_rank=rank, shard_count=shards)
-    eng.set_topology(topo)
-    eng.set_schedule(ev)
     if rank == 0:
         rp, _, _ = topo.csr()
         log(f"[bench] {wl['desc']}: {topo.num_nodes} nodes, {int(rp[-1])} directed entries, "
-            f"{len(ev)} generations in window, setup {time.time() - t_setup:.1f} s")
+            f"{len(ev)} generations in window, {layout}, setup {time.time() - t_setup:.1f} s")
 
-    tick0 = eng.first_tick
-    eng.run(tick0 + W)
-    eng.sync()
-    c0 = eng.counters()
-    eng.reset_timing()
-    if dist:
-        dist.barrier()
-    eng.sync()
-    t0 = time.perf_counter()
-    eng.run(tick0 + W + K)
-    eng.sync()
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    c1 = eng.counters()
-    edges = c1.edge_events - c0.edge_events
-    pull_ms, pull_bytes, launches = c1.pull_ms, c1.pull_bytes, c1.pull_launches
-    gens_done = c1.generations
+    elapsed = 0.0
+    edges = gens_done = launches = 0
+    pull_ms = 0.0
+    acc = dict(moved=0, dense=0, pe=0, col=0, nz=0, srd=0, swr=0, fwr=0)
+    words_hw = words_cap = dev_bytes = 0
+    tick0 = None
+    for s in my_shards:
+        t_eng = time.time()
+        eng = gossip.Engine(n, L_NS, SLICE_NS, T_CUT_NS, device=local, flags=flags,
+                            shard_rank=s, shard_count=shards)
+        eng.set_topology(topo)
+        eng.set_schedule(ev)
+        tick0 = eng.first_tick
+        eng.run(tick0 + W)
+        eng.sync()
+        c0 = eng.counters()
+        eng.reset_timing()
+        if dist:
+            dist.barrier()
+        eng.sync()
+        t0 = time.perf_counter()
+        eng.run(tick0 + W + K)
+        eng.sync()
+        if dist:
+            dist.barrier()
+        t1 = time.perf_counter()
+        c1 = eng.counters()
+        elapsed += t1 - t0
+        edges += c1.edge_events - c0.edge_events
+        gens_done += c1.generations
+        pull_ms += c1.pull_ms
+        launches += c1.pull_launches
+        acc["moved"] += c1.pull_bytes_moved
+        acc["dense"] += c1.pull_bytes
+        acc["pe"] += c1.pull_pair_edges
+        acc["col"] += c1.pull_col_ids
+        acc["nz"] += c1.pull_nz_reads
+        acc["srd"] += c1.pull_seen_reads
+        acc["swr"] += c1.pull_seen_writes
+        acc["fwr"] += c1.pull_f_writes
+        words_hw = max(words_hw, c1.words_hw)
+        words_cap = max(words_cap, c1.words_cap)
+        dev_bytes = max(dev_bytes, c1.device_bytes)
+        eng.close()
+        if rank == 0:
+            log(f"[bench] shard {s} of {shards}: {c1.edge_events - c0.edge_events} edge events in "
+                f"{(t1 - t0) * 1e3:.1f} ms, window {c1.words_hw} words, engine setup + warm-up "
+                f"{t0 - t_eng:.1f} s")
+
     if dist:
         elapsed, pull_ms_max = gd.allreduce_scalars([elapsed, pull_ms], op="max", device=dev)
         edges_total, gens_total = gd.allreduce_scalars([edges, gens_done], op="sum", device=dev)
         edges_total = int(edges_total)
-        # every counted generation of the simulated ticks ran on exactly one rank
+    else:
+        edges_total, gens_total, pull_ms_max = edges, gens_done, pull_ms
+    if not rehearsal:
+        # every counted generation of the simulated ticks ran on exactly one shard
         want = int(np.count_nonzero(ev["ns"] < (tick0 + W + K) * L_NS))
         if int(gens_total) != want:
             raise SystemExit(f"shard coverage broken: {int(gens_total)} generations vs {want}")
-    else:
-        edges_total = edges
-        pull_ms_max = pull_ms
 
     if rank == 0:
         avg_ms = pull_ms / max(launches, 1)
         # Algorithmic bytes per launch of the implemented pull: 16 B per
-        # (edge, word-pair) neighbour read actually needed + 4 B per col index of a pulling
-        # node pass + 16 B per own-row seen/F access + 24 B of per-node row_ptr/counters.
-        bytes_per_launch = c1.pull_bytes_moved / max(launches, 1)
-        dense_bytes_per_launch = pull_bytes / max(launches, 1)  # SURVEY §8d dense formula
-        achieved = bytes_per_launch / (avg_ms * 1e6) if avg_ms > 0 else 0.0  # GB/s
-        traffic = pmc_traffic(wl["name"], n_gpus)
+        # (edge, word-pair) neighbour read actually needed + 4 B per peer id + 8 B per peer
+        # occupancy word + 16 B per own-row seen/F access + per-node row_ptr/counters/occupancy.
         per_launch = lambda x: float(x) / max(launches, 1)  # noqa: E731
+        bytes_per_launch = per_launch(acc["moved"])
+        dense_bytes_per_launch = per_launch(acc["dense"])  # SURVEY §8d dense formula
+        achieved = bytes_per_launch / (avg_ms * 1e6) if avg_ms > 0 else 0.0  # GB/s
         out = {
             "metric": "share-deliveries/sec (edge events)",
             "value": edges_total / elapsed,
@@ -207,16 +249,18 @@ def main():
             "data": "synthetic: G(n,p) by Philox geometric skipping + the reference's mt19937 "
                     "share schedule (node seed + id)",
             "config": {
-                "workload": wl["desc"],
+                "workload": f"{wl['desc']}, {n_gpus} GPU(s), {layout}",
                 "nodes": n,
                 "avg_degree": 16,
                 "latency_ms": 5,
                 "ticks_timed": [tick0 + W, tick0 + W + K],
                 "edge_events_timed": edges_total,
-                "live_words_per_node": c1.words_hw,
-                "window_capacity_words": c1.words_cap,
-                "device_gib": c1.device_bytes / 2**30,
-                "parallelism": f"share-shard x{shards}",
+                "share_shards": shards,
+                "shards_per_gpu": len(my_shards),
+                "live_words_per_node": words_hw,
+                "window_capacity_words": words_cap,
+                "device_gib": dev_bytes / 2**30,
+                "parallelism": f"share-shard x{shards} over {max(world, 1)} rank(s)",
             },
             "roofline": {
                 "bound": "hbm",
@@ -224,34 +268,33 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
+                "traffic": pmc_traffic(wl["name"], n_gpus),
                 "kernel": "k_pull",
                 "bytes_per_launch": bytes_per_launch,
                 "dense_formula_bytes_per_launch": dense_bytes_per_launch,
                 "dense_formula_equiv_gbs": (dense_bytes_per_launch / (avg_ms * 1e6)) if avg_ms > 0 else None,
                 "avg_launch_ms": avg_ms,
+                "launches": launches,
                 "bytes_breakdown_per_launch": {
-                    "peer_rows": per_launch(16 * c1.pull_pair_edges),
-                    "peer_ids": per_launch(4 * c1.pull_col_ids),
-                    "peer_occupancy": per_launch(8 * c1.pull_nz_reads),
-                    "own_seen_read": per_launch(16 * c1.pull_seen_reads),
-                    "own_seen_write": per_launch(16 * c1.pull_seen_writes),
-                    "frontier_write": per_launch(16 * c1.pull_f_writes),
+                    "peer_rows": per_launch(16 * acc["pe"]),
+                    "peer_ids": per_launch(4 * acc["col"]),
+                    "peer_occupancy": per_launch(8 * acc["nz"]),
+                    "own_seen_read": per_launch(16 * acc["srd"]),
+                    "own_seen_write": per_launch(16 * acc["swr"]),
+                    "frontier_write": per_launch(16 * acc["fwr"]),
                     "per_node_rowptr_counters_occupancy": per_launch(
-                        c1.pull_bytes_moved - 16 * c1.pull_pair_edges - 4 * c1.pull_col_ids -
-                        8 * c1.pull_nz_reads - 16 * (c1.pull_seen_reads + c1.pull_seen_writes +
-                                                     c1.pull_f_writes)),
+                        acc["moved"] - 16 * acc["pe"] - 4 * acc["col"] - 8 * acc["nz"] -
+                        16 * (acc["srd"] + acc["swr"] + acc["fwr"])),
                 },
                 "pull_fraction_of_step": (pull_ms_max / (elapsed * 1e3)) if elapsed > 0 else None,
             },
         }
         if n_gpus == 1 and world == 1 and not args.no_cpu_baseline:
             try:
-                out["cpu_baseline"] = cpu_baseline(topo, ev, args.cpu_sample, args.threads)
+                out["cpu_baseline"] = cpu_baseline(topo, ev, args.cpu_sample, args.cpu_hops)
             except Exception as e:  # the baseline is reported, never required
                 out["cpu_baseline"] = {"value": None, "error": str(e)}
         print(json.dumps(out), flush=True)
-    eng.close()
     if dist:
         dist.destroy_process_group()
 

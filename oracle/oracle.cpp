@@ -88,7 +88,6 @@ struct Node {
     std::vector<uint32_t> peers;                  // p2pnode.h:32
     std::unordered_set<uint32_t> peersockets;     // p2pnode.h:39 (keys only)
     std::unordered_set<uint32_t> processed;       // p2pnode.h:38
-    std::mt19937 rng;                             // p2pnode.h:34
     bool running = false;                         // p2pnode.h:36
     uint32_t sent = 0, recv = 0, gen = 0, fwd = 0;  // p2pnode.h:40-43
     uint64_t sent64 = 0;
@@ -106,7 +105,10 @@ struct Event {
 };
 struct EvLater {
     bool operator()(const Event& a, const Event& b) const {
-        return a.t != b.t ? a.t > b.t : a.seq > b.seq;
+        if (a.t != b.t) return a.t > b.t;
+        // a REGISTER runs before any other event of its nanosecond (handshake model only)
+        const int pa = a.type == EV_REGISTER ? 0 : 1, pb = b.type == EV_REGISTER ? 0 : 1;
+        return pa != pb ? pa > pb : a.seq > b.seq;
     }
 };
 
@@ -126,9 +128,13 @@ struct oracle_sim {
     int64_t t_start = 0;      // makeconnections time (5 s)
     int64_t t_cut = 0;        // PrintStatistics time (simTime - 0.1)
     int64_t register_delay = 0;
+    int64_t est_delay = 0;    // handshake model: connector sends before t_start+est are lost
     uint32_t id_mask = 0;
     std::vector<Node> nodes;
-    std::map<std::pair<uint32_t, uint32_t>, int> connections;  // p2pnetwork.cc:30
+    std::vector<std::mt19937> rngs;  // p2pnode.h:34 (reference mode only)
+    // Keys of the `connections` map (p2pnetwork.cc:30) in map order: reference mode builds the
+    // std::map literally and flattens it; replay mode sorts and de-duplicates the given keys.
+    std::vector<std::pair<uint32_t, uint32_t>> links;
     std::vector<Share> shares;
     std::priority_queue<Event, std::vector<Event>, EvLater> q;
     uint64_t seq = 0;
@@ -153,9 +159,6 @@ struct oracle_sim {
         q.push(Event{t, seq++, type, node, arg, hop});
     }
 
-    // ConnectNodes (p2pnetwork.cc:110-130): only the map key matters here.
-    void connect_nodes(uint32_t i, uint32_t j) { connections[std::make_pair(i, j)] = 1; }
-
     // P2PNode::AddPeer (p2pnode.cc:77-83): de-duplicated.
     static void add_peer(Node& nd, uint32_t peer) {
         if (std::find(nd.peers.begin(), nd.peers.end(), peer) == nd.peers.end())
@@ -165,7 +168,7 @@ struct oracle_sim {
     // ScheduleNextShare (p2pnode.cc:97-104): U(2,5) s via libstdc++ generate_canonical.
     void schedule_next_share(Node& nd, int64_t now) {
         std::uniform_real_distribution<double> dist(2.0, 5.0);
-        const double next = dist(nd.rng);
+        const double next = dist(rngs[nd.id]);
         schedule(now + exact_scale_round(next, 1000000000ull), EV_GEN, nd.id, 0, 0);
     }
 
@@ -179,13 +182,17 @@ struct oracle_sim {
     }
 
     // GossipShareToPeers (p2pnode.cc:127-153).  Send never fails at these loads.
+    // Handshake model: before t_start + est_delay only connector-side peers exist and their
+    // sockets are not ESTABLISHED; the share is buffered behind "REGISTER:", which HandleRead
+    // parses as a registration only (p2pnode.cc:178): counted as sent, never delivered.
     void gossip(Node& nd, uint32_t share_idx, int64_t now, uint32_t hop) {
+        const bool lost = est_delay != 0 && now < t_start + est_delay;
         for (uint32_t peer : nd.peers) {
             if (nd.peersockets.find(peer) == nd.peersockets.end()) continue;  // :131-135
             nd.sent++;
             nd.sent64++;
             edge_events++;
-            schedule(now + L, EV_ARRIVE, peer, share_idx, hop + 1);
+            if (!lost) schedule(now + L, EV_ARRIVE, peer, share_idx, hop + 1);
         }
     }
 
@@ -230,8 +237,8 @@ struct oracle_sim {
 
     // makeconnections (p2pnetwork.cc:99-107) -> ConnectPeerSockets (:133-150).
     void on_connect(const Event& e) {
-        for (const auto& kv : connections) {
-            const uint32_t i = kv.first.first, j = kv.first.second;
+        for (const auto& kv : links) {
+            const uint32_t i = kv.first, j = kv.second;
             nodes[i].peersockets.insert(j);  // AddPeerSocket :144
             add_peer(nodes[i], j);           // AddPeer :145
             if (register_delay != 0) schedule(e.t + register_delay, EV_REGISTER, j, i, 0);
@@ -240,8 +247,8 @@ struct oracle_sim {
         // run); HandleRead :178-188 then appends i WITHOUT de-duplication.  The ideal model
         // delivers them at t = 5 s, still after the whole makeconnections loop.
         if (register_delay == 0)
-            for (const auto& kv : connections) {
-                const uint32_t i = kv.first.first, j = kv.first.second;
+            for (const auto& kv : links) {
+                const uint32_t i = kv.first, j = kv.second;
                 nodes[j].peersockets.insert(i);
                 nodes[j].peers.push_back(i);
             }
@@ -297,15 +304,18 @@ int oracle_create_reference(const oracle_params* p, oracle_sim** out) {
     s->t_start = exact_scale_round(5.0, 1000000000ull);      // Seconds(5) :93
     s->t_cut = exact_scale_round(p->sim_time_s - 0.1, 1000000000ull);  // :206
     s->register_delay = p->register_delay_ns;
+    s->est_delay = p->est_delay_ns;
     s->id_mask = p->id_mask;
     s->nodes.resize(s->n);
+    s->rngs.resize(s->n);
     // P2PNode::P2PNode (p2pnode.cc:33-43): rng.seed(rd() + id).
     for (uint32_t i = 0; i < s->n; i++) {
         s->nodes[i].id = i;
-        s->nodes[i].rng.seed((uint32_t)(p->node_seed + i));
+        s->rngs[i].seed((uint32_t)(p->node_seed + i));
     }
-    // CreateRandomTopology (p2pnetwork.cc:62-96).
+    // CreateRandomTopology (p2pnetwork.cc:62-96); ConnectNodes (:110-130) keys the map.
     {
+        std::map<std::pair<uint32_t, uint32_t>, int> connections;  // p2pnetwork.cc:30
         std::mt19937 rng(p->topo_seed);
         std::uniform_real_distribution<double> dist(0.0, 1.0);
         const uint32_t n = s->n;
@@ -314,14 +324,16 @@ int oracle_create_reference(const oracle_params* p, oracle_sim** out) {
             for (uint32_t j = i + 1; j < n; j++) {
                 if (dist(rng) < p->connection_prob) {
                     connected = true;
-                    s->connect_nodes(i, j);
+                    connections[std::make_pair(i, j)] = 1;
                 }
             }
             if (!connected) {
-                if (i == 0) s->connect_nodes(0, 1);
-                else s->connect_nodes(i, i - 1);
+                if (i == 0) connections[std::make_pair(0u, 1u)] = 1;
+                else connections[std::make_pair(i, i - 1)] = 1;
             }
         }
+        s->links.reserve(connections.size());
+        for (const auto& kv : connections) s->links.push_back(kv.first);
     }
     // Event order mirrors the uids the reference hands out: makeconnections is scheduled
     // in CreateRandomTopology (:93), then Start() schedules the first share of every node
@@ -356,10 +368,14 @@ int oracle_create_replay(uint32_t num_nodes, int64_t latency_ns, int64_t t_start
         s->nodes[i].id = i;
         s->nodes[i].running = true;
     }
+    s->links.resize(num_links);
     for (uint64_t k = 0; k < num_links; k++) {
         if (link_a[k] >= num_nodes || link_b[k] >= num_nodes) return fail("link out of range");
-        s->connect_nodes(link_a[k], link_b[k]);
+        s->links[k] = std::make_pair(link_a[k], link_b[k]);
     }
+    // std::map semantics: ordered keys, a repeated key is one entry (p2pnetwork.cc:129).
+    std::sort(s->links.begin(), s->links.end());
+    s->links.erase(std::unique(s->links.begin(), s->links.end()), s->links.end());
     s->rp_ns.assign(ev_ns, ev_ns + num_events);
     s->rp_node.assign(ev_node, ev_node + num_events);
     s->rp_id.assign(ev_id, ev_id + num_events);
@@ -382,6 +398,15 @@ int oracle_create_replay(uint32_t num_nodes, int64_t latency_ns, int64_t t_start
     return 0;
 }
 
+int oracle_set_handshake(oracle_sim* s, int64_t est_delay_ns, int64_t register_delay_ns) {
+    if (!s) return fail("null sim");
+    if (est_delay_ns < 0 || register_delay_ns < 0) return fail("negative delay");
+    if (s->events) return fail("set the handshake model before oracle_run");
+    s->est_delay = est_delay_ns;
+    s->register_delay = register_delay_ns;
+    return 0;
+}
+
 int oracle_enable_trace(oracle_sim* s) {
     if (!s) return fail("null sim");
     s->trace = true;
@@ -396,7 +421,10 @@ int oracle_run(oracle_sim* s) {
         s->q.pop();
         s->events++;
         switch (e.type) {
-            case EV_CONNECT: s->on_connect(e); break;
+            case EV_CONNECT:
+                s->on_connect(e);
+                t0 = std::chrono::steady_clock::now();  // time the gossip, not the peer setup
+                break;
             case EV_GEN: s->on_gen(e); break;
             case EV_ARRIVE: s->on_arrive(e); break;
             case EV_REGISTER: s->on_register(e); break;
@@ -410,6 +438,7 @@ int oracle_run(oracle_sim* s) {
             // frozen at t_cut and zero socket connections (arrivals at closed sockets are
             // not delivered to HandleRead).
             s->on_stats();
+            s->wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             while (!s->q.empty()) {
                 const Event r = s->q.top();
                 s->q.pop();
@@ -427,8 +456,10 @@ int oracle_run(oracle_sim* s) {
             break;
         }
     }
-    if (!s->have_stats) s->on_stats();
-    s->wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!s->have_stats) {
+        s->on_stats();
+        s->wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
     return 0;
 }
 
@@ -458,9 +489,9 @@ int oracle_get_counters(const oracle_sim* s, uint64_t* edge_events, uint64_t* ev
 uint64_t oracle_get_links(const oracle_sim* s, uint32_t* a, uint32_t* b) {
     if (!s) return 0;
     uint64_t k = 0;
-    for (const auto& kv : s->connections) {
-        if (a) a[k] = kv.first.first;
-        if (b) b[k] = kv.first.second;
+    for (const auto& kv : s->links) {
+        if (a) a[k] = kv.first;
+        if (b) b[k] = kv.second;
         k++;
     }
     return k;

@@ -34,6 +34,8 @@ typedef struct oracle_params {
     uint32_t node_seed;        /* replaces rd() at p2pnode.cc:41 (seed+id)     */
     uint32_t id_mask;          /* test knob: shareId &= id_mask (0 => no mask) */
     int64_t register_delay_ns; /* 0 = ideal: REGISTER handled at t=5 s         */
+    int64_t est_delay_ns;      /* handshake model: shares a connector sends before
+                                  t=5 s + est_delay are lost (0 = ideal)        */
 } oracle_params;
 
 /* Build topology + per-node RNGs literally as the reference does. */
@@ -47,6 +49,12 @@ int oracle_create_replay(uint32_t num_nodes, int64_t latency_ns, int64_t t_start
                          const uint32_t* link_b, uint64_t num_events, const int64_t* ev_ns,
                          const uint32_t* ev_node, const uint32_t* ev_id, oracle_sim** out);
 
+/* Handshake model for either mode: shares sent before t_start +
+ * est_delay_ns ride the REGISTER segment and are lost; REGISTER appends the acceptor-side
+ * peer at t_start + register_delay_ns (before any other event of that ns).  Call before
+ * oracle_run. */
+int oracle_set_handshake(oracle_sim* s, int64_t est_delay_ns, int64_t register_delay_ns);
+
 /* Enable the per-(node, shareId) first-contact trace (small runs only). */
 int oracle_enable_trace(oracle_sim* s);
 
@@ -58,7 +66,8 @@ int oracle_run(oracle_sim* s);
 int oracle_get_stats(const oracle_sim* s, uint32_t* gen, uint32_t* recv, uint32_t* fwd,
                      uint64_t* sent, uint32_t* processed, uint32_t* peers, uint32_t* sockets);
 
-/* Totals: edge events (= sum of sends), events processed, wall seconds of oracle_run. */
+/* Totals: edge events (= sum of sends), events processed, wall seconds of the event loop
+ * after makeconnections. */
 int oracle_get_counters(const oracle_sim* s, uint64_t* edge_events, uint64_t* events,
                         double* wall_s);
 

@@ -23,7 +23,7 @@ class oracle_params(C.Structure):
     _fields_ = [
         ("num_nodes", C.c_uint32), ("connection_prob", C.c_double), ("sim_time_s", C.c_double),
         ("latency_ms", C.c_double), ("topo_seed", C.c_uint32), ("node_seed", C.c_uint32),
-        ("id_mask", C.c_uint32), ("register_delay_ns", C.c_int64),
+        ("id_mask", C.c_uint32), ("register_delay_ns", C.c_int64), ("est_delay_ns", C.c_int64),
     ]
 
 
@@ -38,6 +38,7 @@ def load():
         lib.oracle_create_replay.argtypes = [C.c_uint32, C.c_int64, C.c_int64, C.c_int64,
                                              C.c_uint64, P, P, C.c_uint64, P, P, P, C.POINTER(P)]
         lib.oracle_enable_trace.argtypes = [P]
+        lib.oracle_set_handshake.argtypes = [P, C.c_int64, C.c_int64]
         lib.oracle_run.argtypes = [P]
         lib.oracle_get_stats.argtypes = [P] + [P] * 7
         lib.oracle_get_counters.argtypes = [P, P, P, P]
@@ -88,10 +89,10 @@ class OracleSim:
 
     @classmethod
     def reference(cls, num_nodes, connection_prob=0.3, sim_time_s=60.0, latency_ms=5.0,
-                  topo_seed=1, node_seed=1000, id_mask=0, register_delay_ns=0):
+                  topo_seed=1, node_seed=1000, id_mask=0, register_delay_ns=0, est_delay_ns=0):
         lib = load()
         p = oracle_params(num_nodes, connection_prob, sim_time_s, latency_ms, topo_seed, node_seed,
-                          id_mask, register_delay_ns)
+                          id_mask, register_delay_ns, est_delay_ns)
         h = C.c_void_p()
         if lib.oracle_create_reference(C.byref(p), C.byref(h)) != 0:
             raise RuntimeError(lib.oracle_last_error().decode())
@@ -168,8 +169,12 @@ def run_reference(**kw) -> OracleResult:
         s.close()
 
 
-def run_replay(*args, trace=False) -> OracleResult:
+def run_replay(*args, trace=False, handshake=None) -> OracleResult:
+    """handshake = (est_delay_ns, register_delay_ns): the NS-3 handshake-window model."""
     s = OracleSim.replay(*args)
+    if handshake:
+        if load().oracle_set_handshake(s._h, int(handshake[0]), int(handshake[1])) != 0:
+            raise RuntimeError(load().oracle_last_error().decode())
     if trace:
         s.enable_trace()
     try:

@@ -935,8 +935,10 @@ int gossip_engine::tick_step(int64_t t) {
                 while (lpw < 64 && 2 * lpw < (int)c.wact) lpw *= 2;
                 int epn = 1;
                 while (split_edges && lpw * epn * 2 <= 64 && epn * 8 < avg_deg) epn *= 2;
+                // k_pull_wide (scalar peer loop) is opt-in: on C3 it measured 3.41 ms per launch
+                // against 3.33 ms for the lane-shuffle k_pull<64,1> (profiles/r01/ab_generic.json).
                 const bool wide = split_edges && n < (1u << 24) && !(cfg.flags & GOSSIP_F_GENERIC_PULL) &&
-                                  ((lpw == 64 && epn == 1) || (cfg.flags & GOSSIP_F_WIDE_PULL));
+                                  (cfg.flags & GOSSIP_F_WIDE_PULL);
                 if (wide)
                     k_pull_wide<<<grid, 256, pull_lds_bytes(c.wact), stream>>>(c);
                 else

@@ -28,6 +28,9 @@
 //   saturated  -- the node has seen every live column of the pair: peer rows not read;
 //   empty row  -- a peer's 16-word tile row with no frontier bit (its occupancy bit in
 //                 nz_cur is clear) is not read: young tiles are mostly empty rows;
+//   covered    -- once the peer rows read so far hold every bit the node can still take
+//                 (live last tick, unseen, kept) in all words of a tile, the tile's remaining
+//                 peer rows cannot change `new` and are not read (bottom-up early exit);
 //   F_next tile rows are written only when some word of the tile got a bit (and the tile's
 //   occupancy bit set); rows left unwritten hold stale bits that no reader ever loads.
 #pragma once
@@ -47,6 +50,9 @@ constexpr uint32_t kPullLdsWords = 2048;  // words per launch: LDS liveness, new
 #define PULL_INFLIGHT 8
 #endif
 constexpr int kInflight = PULL_INFLIGHT;  // peer-row loads in flight per lane
+#ifndef PULL_EARLY_EXIT
+#define PULL_EARLY_EXIT 1  // 0: read every occupied peer row (A/B build: make variants)
+#endif
 
 __host__ __device__ constexpr size_t pull_lds_bytes(uint32_t wact) {
     return (size_t)wact * 16u + (((size_t)wact + 15u) & ~(size_t)15u);
@@ -201,6 +207,10 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
             } else if (gneed) {  // uniform inside the node group
                 const uint64_t* Fw = a.Fcur + w;
                 if constexpr (EPN == 1) {
+                    // Bits that can still become new (direction-optimising BFS, bottom-up):
+                    // every F_cur bit lies inside live_prev, and seen / not-kept bits are
+                    // masked out of `new`, so peers beyond covering these add nothing.
+                    const uint64_t want0 = lp0 & ~s2.x & k0, want1 = lp1 & ~s2.y & k1;
                     for (int32_t cb = beg; cb < end; cb += GRP) {
                         uint32_t cid = cid0;
                         unsigned long long nzw = nz0;
@@ -215,6 +225,15 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
                         // the <= 8 occupancy bits of this pass's tiles, tested per lane by tile
                         const uint32_t nzp = (uint32_t)(nzw >> ((((w - 2u * wl) >> 4)) & 63u)) & 0xffu;
                         for (int t0 = 0; t0 < rem; t0 += kInflight) {
+                            int open = (a.noskip || !PULL_EARLY_EXIT)
+                                           ? 1 : (((want0 & ~acc0) | (want1 & ~acc1)) != 0ull);
+                            open |= __shfl_xor(open, 1, GRP);  // per tile (8 word-lanes)
+                            open |= __shfl_xor(open, 2, GRP);
+                            open |= __shfl_xor(open, 4, GRP);
+                            int gopen = open;
+#pragma unroll
+                            for (int off = GRP / 2; off > 4; off >>= 1) gopen |= __shfl_xor(gopen, off, GRP);
+                            if (!gopen) break;  // uniform inside the node group
                             uint32_t u[kInflight], z[kInflight];
 #pragma unroll
                             for (int t = 0; t < kInflight; t++) {
@@ -225,7 +244,7 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
 #pragma unroll
                             for (int t = 0; t < kInflight; t++) {
                                 q[t] = make_ulonglong2(0ull, 0ull);
-                                const bool issue = tneed && t0 + t < rem && ((z[t] >> (wl >> 3)) & 1u);
+                                const bool issue = open && tneed && t0 + t < rem && ((z[t] >> (wl >> 3)) & 1u);
                                 if (issue) q[t] = *reinterpret_cast<const ulonglong2*>(Fw + (uint64_t)u[t] * stride);
                                 t_pe += wave_count(issue);
                             }

@@ -35,11 +35,19 @@ def main():
     ap.add_argument("fetch_csv")
     ap.add_argument("write_csv")
     ap.add_argument("--timed", type=int, required=True)
+    ap.add_argument("--passes", type=int, default=1,
+                    help="engine passes in the run (share shards per GPU): the timed "
+                         "dispatches are the last K of each pass")
     ap.add_argument("--kernel", default="k_pull")
     ap.add_argument("--out")
     a = ap.parse_args()
-    f = per_dispatch(a.fetch_csv, "FETCH_SIZE", a.kernel)[-a.timed:]
-    w = per_dispatch(a.write_csv, "WRITE_SIZE", a.kernel)[-a.timed:]
+    def timed(v):  # the last K dispatches of each engine pass
+        P = max(a.passes, 1)
+        per = len(v) // P
+        return [x for q in range(P) for x in v[q * per:(q + 1) * per][-a.timed:]]
+
+    f = timed(per_dispatch(a.fetch_csv, "FETCH_SIZE", a.kernel))
+    w = timed(per_dispatch(a.write_csv, "WRITE_SIZE", a.kernel))
     fetch_kib = sum(f) / max(len(f), 1)
     write_kib = sum(w) / max(len(w), 1)
     out = {

@@ -18,6 +18,9 @@ def main():
     ap.add_argument("prof_dir")
     ap.add_argument("run")
     ap.add_argument("--timed", type=int, required=True)
+    ap.add_argument("--passes", type=int, default=1,
+                    help="engine passes in the run (share shards per GPU): the timed "
+                         "dispatches are the last K of each pass")
     ap.add_argument("--kernel", default="k_pull")
     ap.add_argument("--out")
     a = ap.parse_args()
@@ -25,7 +28,9 @@ def main():
     trace = list(csv.DictReader(open(os.path.join(a.prof_dir, f"{a.run}_kernel_trace.csv"))))
     pulls = [r for r in trace if a.kernel in r["Kernel_Name"]]
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in pulls]
-    timed = dur[-a.timed:]
+    P = max(a.passes, 1)
+    per = len(dur) // P
+    timed = [x for q in range(P) for x in dur[q * per:(q + 1) * per][-a.timed:]]
     out = {
         "kernels": [{"name": r["Name"], "calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                      "total_ms": float(r["TotalDurationNs"]) / 1e6, "pct": float(r["Percentage"])}
