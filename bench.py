@@ -171,7 +171,7 @@ def main():
     words_hw = words_cap = dev_bytes = 0
     tick0 = None
     for s in my_shards:
-        t_eng = time.time()
+        t_eng = time.perf_counter()
         eng = gossip.Engine(n, L_NS, SLICE_NS, T_CUT_NS, device=local, flags=flags,
                             shard_rank=s, shard_count=shards)
         eng.set_topology(topo)

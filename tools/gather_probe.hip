@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
     x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
@@ -45,11 +46,12 @@ void run(const uint4* tab, uint64_t bytes, uint4* out) {
     float ms = 0.f;
     hipEventElapsedTime(&ms, a, b);
     const double moved = 5.0 * grid * 4.0 * iters * 1024.0;
-    printf("{\"row_bytes\": %d, \"GBps\": %.1f}\n", R, moved / (ms * 1e6));
+    printf("{\"table_gib\": %llu, \"row_bytes\": %d, \"GBps\": %.1f}\n", (unsigned long long)(nrows * R >> 30), R, moved / (ms * 1e6));
 }
 
-int main() {
-    const uint64_t bytes = 4ull << 30;
+int main(int argc, char** argv) {
+    // table size in GiB (default 4): random rows over ~100 GB behave like k_pull's frontier rows
+    const uint64_t bytes = (uint64_t)(argc > 1 ? atoi(argv[1]) : 4) << 30;
     uint4* tab = nullptr;
     uint4* out = nullptr;
     if (hipMalloc(&tab, bytes) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
