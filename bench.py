@@ -101,7 +101,7 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1, help="generations in the CPU sample")
-    ap.add_argument("--cpu-hops", type=int, default=5, help="hops the CPU-sample floods run")
+    ap.add_argument("--cpu-hops", type=int, default=6, help="hops the CPU-sample floods run")
     ap.add_argument("--noskip", action="store_true",
                     help="diagnostic: dense pull (every peer-row word read) for PMC calibration")
     ap.add_argument("--pull-kernel", choices=("auto", "wide", "generic"), default="auto",
