@@ -146,6 +146,13 @@ typedef struct gossip_config {
 #define GOSSIP_F_GENERIC_PULL 16u /* diagnostic: lane-shuffle pull kernel at every width     */
 #define GOSSIP_F_TILE_PER_TICK 32u /* test: open a fresh 1024-share tile every tick (wide,
                                       sparsely filled windows at small n)                 */
+#define GOSSIP_F_HANDSHAKE 64u /* NS-3 handshake window (p2pnetwork.cc:133-150,
+                                  p2pnode.cc:178-188): shares a node sends before t_start + 2
+                                  latency ride its REGISTER segment and are lost (still counted
+                                  as sent); until REGISTER arrives at t_start + 3 latency a
+                                  node's peers are its connector-side keys only.  Needs
+                                  gossip_engine_set_topology, CSR mode, t_start % latency == 0
+                                  and t_cut >= t_start + 3 latency.                          */
 
 int gossip_engine_create(const gossip_config* cfg, gossip_engine** out);
 /* Graph: CSR over distinct neighbours with multiplicity in {1,2} (see topology above). */

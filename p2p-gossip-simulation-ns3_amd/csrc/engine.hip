@@ -58,7 +58,8 @@ struct WordCtl {
     uint64_t snap;    // columns whose arrivals count toward the snapshot partial
 };
 
-enum : uint32_t { BIRTH_NOOP = 0, BIRTH_NORMAL = 1, BIRTH_GROUP = 2 };
+enum : uint32_t { BIRTH_NOOP = 0, BIRTH_NORMAL = 1, BIRTH_GROUP = 2, BIRTH_LOST = 3 };
+enum : uint32_t { BF_CONN = 1u };  // Birth::flags: before REGISTER, |peers| = connector-side keys
 
 struct Birth {
     uint32_t node;
@@ -68,7 +69,7 @@ struct Birth {
     uint32_t glo;    // group: first bit in word
     uint32_t glen;   // group: number of bits
     uint32_t poff;   // group: offset of member phases in the per-tick phase buffer
-    uint32_t pad;
+    uint32_t flags;  // BF_*
 };
 
 struct PullArgs {
@@ -168,6 +169,7 @@ struct BirthArgs {
     int64_t snap_r;            // snapshot phase threshold (valid when snap != null)
     unsigned long long* nz;    // tile occupancy of Fnext (nullable: legacy zero-filled rows)
     uint32_t ntw;
+    const uint32_t* degc;      // handshake window: connector-side |peers| (read only with BF_CONN)
 };
 
 // GenerateAndGossipShare (p2pnode.cc:106-125): gen++, insert, send to all peers -- sends and
@@ -180,8 +182,12 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
     const uint64_t v = x.node;
     const uint32_t dv = a.deg[v];
     a.gen[v] += 1u;
-    a.sent[v] += dv;
+    a.sent[v] += (x.flags & BF_CONN) ? a.degc[v] : dv;  // :129-146, peers at this instant
     if (x.kind == BIRTH_NOOP) return;
+    if (x.kind == BIRTH_LOST) {  // sent behind the REGISTER segment (:178): lost, id processed
+        a.effgen[v] += 1u;
+        return;
+    }
     const uint32_t w = x.col >> 6;
     const uint64_t bit = 1ull << (x.col & 63u);
     uint64_t* fp = a.Fnext + v * a.stride + w;
@@ -280,6 +286,12 @@ struct gossip_engine {
     int64_t* d_rowptr = nullptr;
     int32_t* d_col = nullptr;
     uint32_t* d_deg = nullptr;
+    // ---- NS-3 handshake window (GOSSIP_F_HANDSHAKE)
+    bool handshake = false;
+    std::vector<uint32_t> h_degc;   // |peers(v)| before REGISTER arrives = keys (v, *)
+    int64_t* d_rowptr_c = nullptr;  // connector edges a -> b of the keys (a, b), rows b
+    int32_t* d_col_c = nullptr;
+    uint32_t* d_degc = nullptr;
     // ---- schedule (this shard)
     std::vector<gossip_gen_event> ev;   // sorted by ns
     std::vector<uint32_t> ev_inst;      // instance of each event
@@ -384,6 +396,7 @@ gossip_engine::~gossip_engine() {
     for (auto e : event_pool) hipEventDestroy(e);
     // Teardown: errors are ignored (nothing to report them to from a destructor).
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
+    hipFree(d_rowptr_c); hipFree(d_col_c); hipFree(d_degc);
     hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
@@ -828,7 +841,15 @@ int gossip_engine::tick_step(int64_t t) {
         Birth b{};
         b.node = e.node;
         b.phase = (int32_t)(e.ns % L);
-        if (I.state == 2) {
+        // handshake window (tick0 = t_start / L): REGISTER lands at tick0 + 3 before any
+        // other event of that instant, so births up to tick0 + 2 see connector-side peers only
+        if (handshake && t < tick0 + 3) b.flags = BF_CONN;
+        if (handshake && t < tick0 + 2) {
+            // sent before the connector sockets are ESTABLISHED: lost (unique id, checked)
+            b.kind = BIRTH_LOST;
+            I.state = 2;
+            if (trace) tr.push_back(Tr{e.node, e.share_id, t, 0u, (uint8_t)0});
+        } else if (I.state == 2) {
             b.kind = BIRTH_NOOP;
         } else {
             if (I.state == 0) {
@@ -909,6 +930,10 @@ int gossip_engine::tick_step(int64_t t) {
     if (wact) {
         PullArgs a;
         a.rowptr = d_rowptr; a.col = d_col; a.deg = d_deg;
+        if (handshake && t == tick0 + 3) {  // shares sent in [t_start+2L, t_start+3L): a -> b only
+            a.rowptr = d_rowptr_c;
+            a.col = d_col_c;
+        }
         a.Fcur = d_F[fcur]; a.Fnext = d_F[nxt]; a.seen = d_seen; a.ctl = d_ctl[slot];
         a.wflags = d_wflags[slot];
         a.recv = d_recv; a.sent = d_sent; a.live = d_live[lv]; a.snap = snap_ptr;
@@ -998,6 +1023,7 @@ int gossip_engine::tick_step(int64_t t) {
         b.live = d_live[lv]; b.snap = snap_ptr; b.snap_r = snap_idx >= 0 ? snaps[snap_idx].r : 0;
         b.nz = d_nz[nxt];
         b.ntw = ntw;
+        b.degc = d_degc;
         k_births<<<(nb + 255) / 256, 256, 0, stream>>>(b);
         HIP_TRY(hipGetLastError());
     }
@@ -1091,6 +1117,14 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->cur = e->tick0;
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
         e->dense = cfg->mode == GOSSIP_MODE_DENSE;
+        e->handshake = (cfg->flags & GOSSIP_F_HANDSHAKE) != 0;
+        if (e->handshake) {
+            if (e->dense) return set_error(GOSSIP_EINVAL, "GOSSIP_F_HANDSHAKE: CSR mode only");
+            if (e->t0 < 0 || e->t0 % e->L != 0)
+                return set_error(GOSSIP_EINVAL, "GOSSIP_F_HANDSHAKE: t_start must be a multiple of the latency");
+            if (cfg->t_cut_ns < e->t0 + 3 * e->L)
+                return set_error(GOSSIP_EINVAL, "GOSSIP_F_HANDSHAKE: t_cut must be >= t_start + 3 latency");
+        }
         *out = e.release();
         return GOSSIP_OK;
     } catch (const std::bad_alloc&) {
@@ -1173,7 +1207,34 @@ int gossip_engine_set_graph(gossip_engine* e, uint32_t num_nodes, const int64_t*
 
 int gossip_engine_set_topology(gossip_engine* e, const gossip_topology* t) {
     if (!t) return set_error(GOSSIP_EINVAL, "NULL topology");
-    return gossip_engine_set_graph(e, t->n, t->row_ptr.data(), t->col.data(), t->mult.data());
+    int rc = gossip_engine_set_graph(e, t->n, t->row_ptr.data(), t->col.data(), t->mult.data());
+    if (rc || !e->handshake) return rc;
+    // Handshake window: key (a,b) puts b in peers(a) at makeconnections (p2pnetwork.cc:144-145)
+    // and a in peers(b) only when REGISTER arrives (p2pnode.cc:185-186).  Until then v sends
+    // to its |keys (v,*)| connector-side peers, and the shares that get through (sent in
+    // [t_start + 2L, t_start + 3L)) travel a -> b only: a CSR of those edges, rows b.
+    try {
+        const uint32_t n = t->n;
+        std::vector<int64_t> rp((size_t)n + 1, 0);
+        e->h_degc.assign(n, 0);
+        for (size_t k = 0; k < t->la.size(); k++) {
+            e->h_degc[t->la[k]]++;
+            rp[(size_t)t->lb[k] + 1]++;
+        }
+        for (uint32_t v = 0; v < n; v++) rp[v + 1] += rp[v];
+        std::vector<int32_t> col((size_t)rp[n]);
+        std::vector<int64_t> pos(rp.begin(), rp.end() - 1);
+        for (size_t k = 0; k < t->la.size(); k++) col[(size_t)pos[t->lb[k]]++] = (int32_t)t->la[k];
+        HIP_TRY(hipMalloc(&e->d_rowptr_c, ((size_t)n + 1) * 8));
+        HIP_TRY(hipMalloc(&e->d_col_c, std::max<size_t>(col.size(), 1) * 4));
+        HIP_TRY(hipMalloc(&e->d_degc, (size_t)std::max<uint32_t>(n, 1) * 4));
+        HIP_TRY(hipMemcpy(e->d_rowptr_c, rp.data(), rp.size() * 8, hipMemcpyHostToDevice));
+        if (!col.empty()) HIP_TRY(hipMemcpy(e->d_col_c, col.data(), col.size() * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(e->d_degc, e->h_degc.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    } catch (const std::bad_alloc&) {
+        return set_error(GOSSIP_ENOMEM, "host allocation failed");
+    }
+    return GOSSIP_OK;
 }
 
 int gossip_engine_add_snapshot(gossip_engine* e, int64_t t_ns) {
@@ -1204,6 +1265,36 @@ int gossip_engine_set_schedule(gossip_engine* e, uint64_t num_events, const goss
         for (uint64_t k = 1; k < e->ev.size(); k++)
             if (e->ev[k].node == e->ev[k - 1].node && e->ev[k].ns == e->ev[k - 1].ns)
                 return set_error(GOSSIP_EINVAL, "duplicate generation event");
+        if (e->handshake && e->h_degc.empty())
+            return set_error(GOSSIP_ESTATE, "GOSSIP_F_HANDSHAKE needs the link keys: use gossip_engine_set_topology");
+        // GenerateAndGossipShare's peers.empty() branch (p2pnode.cc:108-113): a generation at a
+        // node without peers is not counted (before REGISTER only connector-side peers exist).
+        {
+            const int64_t t_reg = e->t0 + 3 * e->L;
+            size_t o = 0;
+            for (size_t k = 0; k < e->ev.size(); k++) {
+                const gossip_gen_event& x = e->ev[k];
+                const bool no_peers = e->h_peers[x.node] == 0 ||
+                                      (e->handshake && x.ns < t_reg && e->h_degc[x.node] == 0);
+                if (!no_peers) e->ev[o++] = x;
+            }
+            e->ev.resize(o);
+        }
+        if (e->handshake) {
+            // A share sent before t_start + 2L is lost with its REGISTER segment and floods
+            // nothing; its id must not belong to another generation the engine would merge.
+            const int64_t t_est = e->t0 + 2 * e->L;
+            std::vector<uint32_t> ids(e->ev.size());
+            for (size_t k = 0; k < e->ev.size(); k++) ids[k] = e->ev[k].share_id;
+            std::sort(ids.begin(), ids.end());
+            for (const auto& x : e->ev) {
+                if (x.ns >= t_est) break;  // sorted by ns
+                const auto r = std::equal_range(ids.begin(), ids.end(), x.share_id);
+                if (r.second - r.first > 1)
+                    return set_error(GOSSIP_EINVAL, "GOSSIP_F_HANDSHAKE: a share lost in the handshake "
+                                                    "window shares its id with another generation");
+            }
+        }
         int rc = e->prepare_instances();
         if (rc) return rc;
         for (auto& s : e->snaps) {

@@ -34,6 +34,7 @@ struct Options {
     bool quiet = false;                // totals only (no per-node lines)
     bool periodic = true;
     bool timing = false;
+    bool handshake = false;            // NS-3 handshake window (GOSSIP_F_HANDSHAKE)
     std::string dumpLinks, dumpEvents, linksIn, eventsIn;
 };
 
@@ -43,7 +44,7 @@ void usage() {
                  "[--Latency=MS]\n"
                  "                  [--seed=S] [--nodeSeed=S] [--topology=auto|exact|skip]\n"
                  "                  [--device=D] [--threads=T] [--maxWords=W] [--quiet]\n"
-                 "                  [--noPeriodic] [--timing] [--dumpLinks=F] [--dumpEvents=F]\n"
+                 "                  [--noPeriodic] [--timing] [--handshake] [--dumpLinks=F] [--dumpEvents=F]\n"
                  "                  [--links=F] [--events=F]\n");
 }
 
@@ -96,6 +97,7 @@ bool parse(int argc, char** argv, Options& o) {
         else if (key == "quiet") o.quiet = true;
         else if (key == "noPeriodic") o.periodic = false;
         else if (key == "timing") o.timing = true;
+        else if (key == "handshake") o.handshake = true;
         else if (key == "dumpLinks") { if (!need()) return false; o.dumpLinks = val; }
         else if (key == "dumpEvents") { if (!need()) return false; o.dumpEvents = val; }
         else if (key == "links") { if (!need()) return false; o.linksIn = val; }
@@ -187,7 +189,7 @@ int main(int argc, char** argv) {
     cfg.device = o.device;
     cfg.mode = GOSSIP_MODE_AUTO;
     cfg.max_words = o.maxWords;
-    cfg.flags = o.timing ? GOSSIP_F_TIMING : 0u;
+    cfg.flags = (o.timing ? GOSSIP_F_TIMING : 0u) | (o.handshake ? GOSSIP_F_HANDSHAKE : 0u);
     gossip_engine* eng = nullptr;
     if (gossip_engine_create(&cfg, &eng)) return die("engine create");
     if (gossip_engine_set_topology(eng, topo)) return die("engine graph");
