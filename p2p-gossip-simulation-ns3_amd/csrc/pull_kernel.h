@@ -47,7 +47,7 @@ enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u };
 
 constexpr uint32_t kPullLdsWords = 2048;  // words per launch: LDS liveness, new liveness, flags
 #ifndef PULL_INFLIGHT
-#define PULL_INFLIGHT 8
+#define PULL_INFLIGHT 8  // A/B builds: make variants (q4, q16)
 #endif
 constexpr int kInflight = PULL_INFLIGHT;  // peer-row loads in flight per lane
 #ifndef PULL_EARLY_EXIT
