@@ -146,6 +146,14 @@ typedef struct gossip_config {
 #define GOSSIP_F_GENERIC_PULL 16u /* diagnostic: lane-shuffle pull kernel at every width     */
 #define GOSSIP_F_TILE_PER_TICK 32u /* test: open a fresh 1024-share tile every tick (wide,
                                       sparsely filled windows at small n)                 */
+#define GOSSIP_F_HOP_BATCH 128u /* hop-batched run: generation g of every node is simulated in
+                                   batched tick g (its phase kept) and the cut / snapshots are
+                                   applied per share from the real times -- exact when no two
+                                   generations share an id (n <= 128,849; EINVAL otherwise).
+                                   Thousands of concurrent shares per step instead of a few:
+                                   the dense (MFMA) path's mode for small graphs.  The run ends
+                                   when every flood has retired (end_tick is not meaningful);
+                                   snapshots are read after the complete run.                  */
 #define GOSSIP_F_HANDSHAKE 64u /* NS-3 handshake window (p2pnetwork.cc:133-150,
                                   p2pnode.cc:178-188): shares a node sends before t_start + 2
                                   latency ride its REGISTER segment and are lost (still counted

@@ -239,6 +239,35 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
     }
 }
 
+// Hop-batched snapshots: out[2 + 2s + 1] += popcount(F[v][w] & mask[s][w]) over the frontier
+// rows whose tile occupancy bit is set (other rows hold stale bits).  mask[s] holds the columns
+// whose arrival in this batched tick happened before snapshot s in real time (hop >= 1).
+constexpr uint32_t kSnapGroup = 8;
+__global__ __launch_bounds__(256) void k_snap_count(const uint64_t* __restrict__ F,
+                                                    const unsigned long long* __restrict__ nz,
+                                                    uint32_t stride, uint32_t ntw, uint32_t n,
+                                                    uint32_t hw, const uint64_t* __restrict__ mask,
+                                                    uint32_t s0, uint32_t ns,
+                                                    unsigned long long* out) {
+    unsigned long long acc[kSnapGroup] = {};
+    const uint64_t total = (uint64_t)n * hw;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256u) {
+        const uint32_t v = (uint32_t)(i / hw), w = (uint32_t)(i % hw), tile = w >> 4;
+        if (!((nz[(uint64_t)v * ntw + (tile >> 6)] >> (tile & 63u)) & 1ull)) continue;
+        const uint64_t x = F[(uint64_t)v * stride + w];
+        if (!x) continue;
+#pragma unroll
+        for (uint32_t s = 0; s < kSnapGroup; s++)
+            if (s < ns) acc[s] += (unsigned long long)__popcll(x & mask[(uint64_t)(s0 + s) * hw + w]);
+    }
+#pragma unroll
+    for (uint32_t s = 0; s < kSnapGroup; s++) {
+        unsigned long long x = acc[s];
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        if ((threadIdx.x & 63u) == 0 && s < ns && x) atomicAdd(&out[2 + 2 * (s0 + s) + 1], x);
+    }
+}
+
 // sum over nodes of (a[v] + b[v]) (b nullable) into *out (64-bit).
 __global__ __launch_bounds__(256) void k_sum_u32(const uint32_t* a, const uint32_t* b, uint32_t n,
                                                  unsigned long long* out) {
@@ -292,6 +321,13 @@ struct gossip_engine {
     int64_t* d_rowptr_c = nullptr;  // connector edges a -> b of the keys (a, b), rows b
     int32_t* d_col_c = nullptr;
     uint32_t* d_degc = nullptr;
+    // ---- hop batching (GOSSIP_F_HOP_BATCH): generation g of every node is born in batched
+    // tick tick0 + 1 + g (phase kept); per-column cut / snapshot masks use the real times
+    bool batch = false, done = false;
+    int64_t last_birth_tick = -1;
+    std::vector<int64_t> ev_orig_ns;      // real generation time of ev[k]
+    uint64_t* d_smask[4] = {};            // per ring slot: snapshot masks [snap][word]
+    uint64_t* h_smask[4] = {};
     // ---- schedule (this shard)
     std::vector<gossip_gen_event> ev;   // sorted by ns
     std::vector<uint32_t> ev_inst;      // instance of each event
@@ -397,6 +433,7 @@ gossip_engine::~gossip_engine() {
     // Teardown: errors are ignored (nothing to report them to from a destructor).
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
     hipFree(d_rowptr_c); hipFree(d_col_c); hipFree(d_degc);
+    for (int k = 0; k < 4; k++) { hipFree(d_smask[k]); hipHostFree(h_smask[k]); }
     hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
@@ -499,16 +536,19 @@ int gossip_engine::prepare_instances() {
     ev2.reserve(m);
     ev_inst.clear();
     ev_rank.clear();
+    std::vector<int64_t> orig2;
     for (uint64_t q = 0; q < m; q++) {
         if (!keep[q]) continue;
         newidx[q] = (uint32_t)ev2.size();
         ev2.push_back(ev[q]);
+        if (!ev_orig_ns.empty()) orig2.push_back(ev_orig_ns[q]);
         ev_inst.push_back(inst_of[q]);
         ev_rank.push_back(rank_of[q]);
     }
     for (auto& x : grp_members) x = newidx[x];
     for (auto& I : inst) I.first_ev = newidx[I.first_ev];
     ev.swap(ev2);
+    if (!ev_orig_ns.empty()) ev_orig_ns.swap(orig2);
     // Tick buckets.
     const int64_t nt = tick_end - tick0 + 1;
     tick_lo.assign((size_t)nt + 1, 0);
@@ -653,6 +693,11 @@ int gossip_engine::alloc_device() {
         HIP_TRY(hipMemsetAsync(d_inc, 0, bm, stream));
         device_bytes += ft + bm + (uint64_t)n_pad * n_pad / 8;
     }
+    if (batch && !snaps.empty())
+        for (int k = 0; k < kRing; k++) {
+            HIP_TRY(hipMalloc(&d_smask[k], (size_t)stride * snaps.size() * 8));
+            HIP_TRY(hipHostMalloc(&h_smask[k], (size_t)stride * snaps.size() * 8, hipHostMallocDefault));
+        }
     WordCtl z{0ull, ~0ull, 0ull, 0ull, 0ull};
     ctl.assign(stride, z);
     tile_alloc.assign(stride / kTileWords, 0);
@@ -741,6 +786,13 @@ int gossip_engine::grow(uint32_t new_stride) {
         HIP_TRY(hipMemset(d_inc, 0, nb));
         device_bytes += (uint64_t)(new_stride - stride) * (8ull * n_pad + 8ull * n);
     }
+    if (batch && !snaps.empty())
+        for (int k = 0; k < kRing; k++) {  // rebuilt every tick: no copy
+            HIP_TRY(hipFree(d_smask[k]));
+            HIP_TRY(hipHostFree(h_smask[k]));
+            HIP_TRY(hipMalloc(&d_smask[k], (size_t)new_stride * snaps.size() * 8));
+            HIP_TRY(hipHostMalloc(&h_smask[k], (size_t)new_stride * snaps.size() * 8, hipHostMallocDefault));
+        }
     WordCtl z{0ull, ~0ull, 0ull, 0ull, 0ull};
     ctl.resize(new_stride, z);
     tile_alloc.resize(new_stride / kTileWords, 0);
@@ -832,7 +884,9 @@ int gossip_engine::tick_step(int64_t t) {
     // 3. births of tick t
     reset_now.clear();
     uint32_t nb = 0, np = 0;
-    const uint64_t lo = tick_lo[(size_t)(t - tick0)], hi = tick_lo[(size_t)(t - tick0) + 1];
+    // (hop-batched runs keep stepping after the last birth tick until the floods retire)
+    const size_t tb = (size_t)(t - tick0);
+    const uint64_t lo = tb + 1 < tick_lo.size() ? tick_lo[tb] : 0, hi = tb + 1 < tick_lo.size() ? tick_lo[tb + 1] : 0;
     Birth* B = h_births[slot];
     int32_t* GP = h_gphase[slot];
     for (uint64_t q = lo; q < hi; q++) {
@@ -895,13 +949,36 @@ int gossip_engine::tick_step(int64_t t) {
     for (uint32_t w : reset_now) ctl[w].clear = ~0ull;
     const bool is_cut = (t == cut_tick && cut_r > 0);
     int snap_idx = -1;
-    for (size_t s = 0; s < snaps.size(); s++)
+    for (size_t s = 0; s < snaps.size() && !batch; s++)
         if (snaps[s].tick == t && snaps[s].r > 0) snap_idx = (int)s;
     WordCtl* C = h_ctl[slot];
     uint8_t* WF = h_wflags[slot];
+    const size_t nsnap = batch ? snaps.size() : 0;
+    bool smask_any = false;
+    if (nsnap && hw) std::memset(h_smask[slot], 0, (size_t)nsnap * hw * 8);
     for (uint32_t w = 0; w < hw; w++) {
         WordCtl c = ctl[w];
-        if (is_cut || snap_idx >= 0) {
+        if (batch) {
+            // column c (generation at real time tb, batched birth tick bt) is at hop t - bt: its
+            // arrival counts iff tb + hop*L < t_cut (PrintStatistics), and toward snapshot s
+            // iff tb + hop*L < T_s
+            uint64_t km = 0ull;
+            for (int bb = 0; bb < 64; bb++) {
+                const uint32_t q = col_src[(size_t)w * 64 + bb];
+                if (q == UINT32_MAX) {
+                    km |= 1ull << bb;
+                    continue;
+                }
+                const int64_t hop = t - ev[q].ns / L, ta = ev_orig_ns[q] + hop * L;
+                if (ta < cfg.t_cut_ns) km |= 1ull << bb;
+                for (size_t s = 0; s < nsnap; s++)
+                    if (hop >= 1 && ta < snaps[s].t_ns) {
+                        h_smask[slot][s * hw + w] |= 1ull << bb;
+                        smask_any = true;
+                    }
+            }
+            c.keep = km;
+        } else if (is_cut || snap_idx >= 0) {
             uint64_t km = 0ull, sm = 0ull;
             for (int bb = 0; bb < 64; bb++) {
                 const int32_t ph = col_phase[(size_t)w * 64 + bb];
@@ -922,6 +999,7 @@ int gossip_engine::tick_step(int64_t t) {
     if (wact) HIP_TRY(hipMemcpyAsync(d_wflags[slot], WF, (size_t)wact, hipMemcpyHostToDevice, stream));
     if (nb) HIP_TRY(hipMemcpyAsync(d_births[slot], B, (size_t)nb * sizeof(Birth), hipMemcpyHostToDevice, stream));
     if (np) HIP_TRY(hipMemcpyAsync(d_gphase[slot], GP, (size_t)np * 4, hipMemcpyHostToDevice, stream));
+    if (smask_any) HIP_TRY(hipMemcpyAsync(d_smask[slot], h_smask[slot], nsnap * hw * 8, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipEventRecord(slot_done[slot], stream));
     const int lv = (int)(t % 3);
     if (wact) HIP_TRY(hipMemsetAsync(d_live[lv], 0, (size_t)wact * 8, stream));
@@ -1027,6 +1105,15 @@ int gossip_engine::tick_step(int64_t t) {
         k_births<<<(nb + 255) / 256, 256, 0, stream>>>(b);
         HIP_TRY(hipGetLastError());
     }
+    if (smask_any) {  // hop-batched snapshots: arrivals of this tick that precede each snapshot
+        const uint64_t cells = (uint64_t)n * hw;
+        const uint32_t g = (uint32_t)std::min<uint64_t>((cells + 255) / 256, 4096);
+        for (uint32_t s0 = 0; s0 < nsnap; s0 += kSnapGroup) {
+            k_snap_count<<<g, 256, 0, stream>>>(d_F[nxt], d_nz[nxt], stride, ntw, n, hw, d_smask[slot], s0,
+                                                (uint32_t)std::min<size_t>(kSnapGroup, nsnap - s0), d_scalars);
+            HIP_TRY(hipGetLastError());
+        }
+    }
     // 6. liveness read-back (consumed kLag ticks later)
     {
         const int ls = (int)(t % kRing);
@@ -1039,7 +1126,7 @@ int gossip_engine::tick_step(int64_t t) {
     }
     // 7. snapshot bases: totals over ticks < snap.tick (the partial of snap.tick, if any,
     //    is accumulated by that tick's pull/births through ctl.snap)
-    for (size_t s = 0; s < snaps.size(); s++) {
+    for (size_t s = 0; s < snaps.size() && !batch; s++) {
         if (snaps[s].tick == t + 1) {
             k_sum_u32<<<256, 256, 0, stream>>>(d_recv, d_effgen, n, d_scalars + 2 + 2 * s);
             HIP_TRY(hipGetLastError());
@@ -1077,7 +1164,8 @@ int gossip_engine::decode_trace(int64_t t) {
                 const gossip_gen_event& e = ev[src];
                 const int64_t bt = e.ns / L;
                 const bool birth = (e.node == v && bt == t);
-                tr.push_back(Tr{v, e.share_id, t, (uint32_t)(t - bt), (uint8_t)(birth ? 0 : 1)});
+                const int64_t real_t = batch ? ev_orig_ns[src] / L + (t - bt) : t;
+                tr.push_back(Tr{v, e.share_id, real_t, (uint32_t)(t - bt), (uint8_t)(birth ? 0 : 1)});
             }
         }
     return GOSSIP_OK;
@@ -1118,6 +1206,9 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
         e->dense = cfg->mode == GOSSIP_MODE_DENSE;
         e->handshake = (cfg->flags & GOSSIP_F_HANDSHAKE) != 0;
+        e->batch = (cfg->flags & GOSSIP_F_HOP_BATCH) != 0;
+        if (e->batch && e->handshake)
+            return set_error(GOSSIP_EINVAL, "GOSSIP_F_HOP_BATCH and GOSSIP_F_HANDSHAKE are exclusive");
         if (e->handshake) {
             if (e->dense) return set_error(GOSSIP_EINVAL, "GOSSIP_F_HANDSHAKE: CSR mode only");
             if (e->t0 < 0 || e->t0 % e->L != 0)
@@ -1295,16 +1386,44 @@ int gossip_engine_set_schedule(gossip_engine* e, uint64_t num_events, const goss
                                                     "window shares its id with another generation");
             }
         }
+        if (e->batch) {
+            // Shares are independent floods when no two generations share an id (the seen set
+            // is keyed by id, p2pnode.cc:189), so each can run at any tick: generation g of a
+            // node moves to tick tick0 + 1 + g with its phase.  Exact: counts depend only on
+            // hops, and the cut / snapshots are applied per column from the real times.
+            if (gossip::any_id_collision(e->ev.size(), e->ev.data()))
+                return set_error(GOSSIP_EINVAL, "GOSSIP_F_HOP_BATCH needs unique share ids (n <= 128,849)");
+            std::vector<uint32_t> gi(e->n, 0);
+            std::vector<std::pair<gossip_gen_event, int64_t>> rm(e->ev.size());
+            for (size_t k = 0; k < e->ev.size(); k++) {
+                gossip_gen_event x = e->ev[k];
+                const int64_t orig = x.ns;
+                x.ns = (e->tick0 + 1 + (int64_t)gi[x.node]++) * e->L + orig % e->L;
+                rm[k] = {x, orig};
+            }
+            std::stable_sort(rm.begin(), rm.end(), [](const auto& a, const auto& b) {
+                return a.first.ns != b.first.ns ? a.first.ns < b.first.ns : a.first.node < b.first.node;
+            });
+            e->ev_orig_ns.resize(rm.size());
+            for (size_t k = 0; k < rm.size(); k++) {
+                e->ev[k] = rm[k].first;
+                e->ev_orig_ns[k] = rm[k].second;
+            }
+            e->last_birth_tick = e->ev.empty() ? e->tick0 : e->ev.back().ns / e->L;
+            e->cut_tick = -1;  // per-column cut instead
+            e->tick_end = e->last_birth_tick + 1;
+        }
         int rc = e->prepare_instances();
         if (rc) return rc;
         for (auto& s : e->snaps) {
             uint64_t g = 0;
-            for (const auto& x : e->ev)
-                if (x.ns < s.t_ns) g++;
+            for (size_t k = 0; k < e->ev.size(); k++)
+                if ((e->batch ? e->ev_orig_ns[k] : e->ev[k].ns) < s.t_ns) g++;
             s.gen_total = g;
         }
         rc = e->alloc_device();
         if (rc) return rc;
+        if (e->batch) e->tick_end = INT64_MAX / 4;  // runs until every flood has retired
     } catch (const std::bad_alloc&) {
         return set_error(GOSSIP_ENOMEM, "host allocation failed");
     }
@@ -1328,6 +1447,11 @@ int gossip_engine_run(gossip_engine* e, int64_t tick_end) {
     if (tick_end > e->tick_end) tick_end = e->tick_end;
     try {
         while (e->cur < tick_end) {
+            if (e->batch && e->cur > e->last_birth_tick &&
+                std::find(e->tile_alloc.begin(), e->tile_alloc.end(), (uint8_t)1) == e->tile_alloc.end()) {
+                e->done = true;
+                break;
+            }
             int rc = e->tick_step(e->cur);
             if (rc) return rc;
             e->cur++;
@@ -1376,10 +1500,11 @@ int gossip_engine_get_snapshot(gossip_engine* e, uint32_t k, int64_t* t_ns, uint
     HIP_TRY(hipSetDevice(e->device));
     if (t_ns) *t_ns = s.t_ns;
     if (total_gen) *total_gen = s.gen_total;
+    if (e->batch && !e->done) return set_error(GOSSIP_ESTATE, "hop-batched snapshots need the complete run");
     if (s.t_ns > e->cfg.t_cut_ns) {
         // After PrintStatistics + StopAllNodes: counters frozen at t_cut (the caller reports
         // zero socket connections, p2pnode.cc:55-69).
-        if (e->cur < e->tick_end) return set_error(GOSSIP_ESTATE, "snapshot after t_cut needs the full run");
+        if (!e->batch && e->cur < e->tick_end) return set_error(GOSSIP_ESTATE, "snapshot after t_cut needs the full run");
         HIP_TRY(hipMemsetAsync(e->d_scalars, 0, 8, e->stream));
         k_sum_u32<<<256, 256, 0, e->stream>>>(e->d_recv, e->d_effgen, e->n, e->d_scalars);
         HIP_TRY(hipGetLastError());
@@ -1389,11 +1514,15 @@ int gossip_engine_get_snapshot(gossip_engine* e, uint32_t k, int64_t* t_ns, uint
         if (total_processed) *total_processed = v;
         return GOSSIP_OK;
     }
-    if (e->cur <= s.tick - (s.r ? 0 : 1) && s.tick >= e->tick0)
+    if (!e->batch && e->cur <= s.tick - (s.r ? 0 : 1) && s.tick >= e->tick0)
         return set_error(GOSSIP_ESTATE, "snapshot time not simulated yet");
     HIP_TRY(hipStreamSynchronize(e->stream));
     unsigned long long v[2] = {0, 0};
     HIP_TRY(hipMemcpy(v, e->d_scalars + 2 + 2 * k, 16, hipMemcpyDeviceToHost));
+    if (e->batch) {  // generations before T (all effective: unique ids) + arrivals before T
+        if (total_processed) *total_processed = s.gen_total + v[1];
+        return GOSSIP_OK;
+    }
     if (total_processed) *total_processed = (s.tick <= e->tick0 && s.r == 0) ? 0 : (v[0] + v[1]);
     return GOSSIP_OK;
 }

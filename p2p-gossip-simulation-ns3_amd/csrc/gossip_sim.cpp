@@ -35,6 +35,8 @@ struct Options {
     bool periodic = true;
     bool timing = false;
     bool handshake = false;            // NS-3 handshake window (GOSSIP_F_HANDSHAKE)
+    bool hopBatch = false;             // hop-batched run (GOSSIP_F_HOP_BATCH)
+    std::string mode = "auto";         // auto | csr | dense
     std::string dumpLinks, dumpEvents, linksIn, eventsIn;
 };
 
@@ -44,7 +46,7 @@ void usage() {
                  "[--Latency=MS]\n"
                  "                  [--seed=S] [--nodeSeed=S] [--topology=auto|exact|skip]\n"
                  "                  [--device=D] [--threads=T] [--maxWords=W] [--quiet]\n"
-                 "                  [--noPeriodic] [--timing] [--handshake] [--dumpLinks=F] [--dumpEvents=F]\n"
+                 "                  [--noPeriodic] [--timing] [--handshake] [--hopBatch]\n                  [--mode=auto|csr|dense] [--dumpLinks=F] [--dumpEvents=F]\n"
                  "                  [--links=F] [--events=F]\n");
 }
 
@@ -98,6 +100,8 @@ bool parse(int argc, char** argv, Options& o) {
         else if (key == "noPeriodic") o.periodic = false;
         else if (key == "timing") o.timing = true;
         else if (key == "handshake") o.handshake = true;
+        else if (key == "hopBatch") o.hopBatch = true;
+        else if (key == "mode") { if (!need()) return false; o.mode = val; }
         else if (key == "dumpLinks") { if (!need()) return false; o.dumpLinks = val; }
         else if (key == "dumpEvents") { if (!need()) return false; o.dumpEvents = val; }
         else if (key == "links") { if (!need()) return false; o.linksIn = val; }
@@ -187,9 +191,13 @@ int main(int argc, char** argv) {
     cfg.t_start_ns = t_start;
     cfg.t_cut_ns = t_cut;
     cfg.device = o.device;
-    cfg.mode = GOSSIP_MODE_AUTO;
+    if (o.mode == "csr") cfg.mode = GOSSIP_MODE_CSR;
+    else if (o.mode == "dense") cfg.mode = GOSSIP_MODE_DENSE;
+    else if (o.mode == "auto") cfg.mode = GOSSIP_MODE_AUTO;
+    else { usage(); return 2; }
     cfg.max_words = o.maxWords;
-    cfg.flags = (o.timing ? GOSSIP_F_TIMING : 0u) | (o.handshake ? GOSSIP_F_HANDSHAKE : 0u);
+    cfg.flags = (o.timing ? GOSSIP_F_TIMING : 0u) | (o.handshake ? GOSSIP_F_HANDSHAKE : 0u) |
+                (o.hopBatch ? GOSSIP_F_HOP_BATCH : 0u);
     gossip_engine* eng = nullptr;
     if (gossip_engine_create(&cfg, &eng)) return die("engine create");
     if (gossip_engine_set_topology(eng, topo)) return die("engine graph");
@@ -202,9 +210,13 @@ int main(int argc, char** argv) {
     if (gossip_engine_set_schedule_obj(eng, sched)) return die("engine schedule");
 
     std::printf("Starting gossip network simulation for %g seconds\n", o.simTime);
-    std::printf("seeds: topology %u, nodes %u; latency %lld ns; ticks [%lld, %lld)\n", o.seed,
-                o.nodeSeed, (long long)L, (long long)gossip_engine_first_tick(eng),
-                (long long)gossip_engine_end_tick(eng));
+    if (o.hopBatch)
+        std::printf("seeds: topology %u, nodes %u; latency %lld ns; hop-batched from tick %lld\n", o.seed,
+                    o.nodeSeed, (long long)L, (long long)gossip_engine_first_tick(eng));
+    else
+        std::printf("seeds: topology %u, nodes %u; latency %lld ns; ticks [%lld, %lld)\n", o.seed,
+                    o.nodeSeed, (long long)L, (long long)gossip_engine_first_tick(eng),
+                    (long long)gossip_engine_end_tick(eng));
     auto w0 = std::chrono::steady_clock::now();
     if (gossip_engine_run(eng, gossip_engine_end_tick(eng))) return die("engine run");
     if (gossip_engine_sync(eng)) return die("engine sync");

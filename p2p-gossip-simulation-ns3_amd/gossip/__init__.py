@@ -37,6 +37,7 @@ F_WIDE_PULL = 8
 F_GENERIC_PULL = 16
 F_TILE_PER_TICK = 32
 F_HANDSHAKE = 64
+F_HOP_BATCH = 128
 
 EXPORTED_SYMBOLS = (
     "gossip_last_error", "gossip_version", "gossip_seconds_to_ns", "gossip_milliseconds_to_ns",

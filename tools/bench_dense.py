@@ -3,6 +3,7 @@
 bit-sliced CSR pull (GOSSIP_MODE_CSR) on the same dense workload.  One JSON line per run.
 
     python tools/bench_dense.py c2            # C2: 4,096 nodes, p=0.3, full 60 s, real time
+    python tools/bench_dense.py c2 --batch    # the same run hop-batched (GOSSIP_F_HOP_BATCH)
     python tools/bench_dense.py c5 --width 512 # C5 slice: 65,536 nodes, p=0.3, one flood batch
                                                # of `width` concurrent shares, 1 GPU
 
@@ -25,8 +26,8 @@ T0, L = 5_000_000_000, 5_000_000
 INT8_PEAK_OPS = 5.0e15
 
 
-def run(topo, ev, t_cut, mode, tick_end=None):
-    eng = gossip.Engine(topo.num_nodes, L, T0, t_cut, mode=mode, flags=gossip.F_TIMING)
+def run(topo, ev, t_cut, mode, tick_end=None, flags=0):
+    eng = gossip.Engine(topo.num_nodes, L, T0, t_cut, mode=mode, flags=gossip.F_TIMING | flags)
     eng.set_topology(topo)
     eng.set_schedule(ev)
     eng.reset_timing()
@@ -46,6 +47,7 @@ def main():
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--nodes", type=int, default=0)
     ap.add_argument("--modes", default="csr,dense")
+    ap.add_argument("--batch", action="store_true", help="hop-batched run (GOSSIP_F_HOP_BATCH)")
     a = ap.parse_args()
     if a.config == "c2":
         n = a.nodes or 4096
@@ -67,12 +69,12 @@ def main():
     ref = None
     for mode in a.modes.split(","):
         m = gossip.MODE_DENSE if mode == "dense" else gossip.MODE_CSR
-        wall, c, st = run(topo, ev, t_cut, m)
+        wall, c, st = run(topo, ev, t_cut, m, flags=gossip.F_HOP_BATCH if a.batch else 0)
         if ref is None:
             ref = st
         same = all(np.array_equal(getattr(st, k), getattr(ref, k))
                    for k in ("gen", "recv", "sent", "processed"))
-        out = {"workload": desc, "mode": mode, "wall_s": wall, "ticks": c.ticks,
+        out = {"workload": desc, "mode": mode + (" hop-batched" if a.batch else ""), "wall_s": wall, "ticks": c.ticks,
                "edge_events": c.edge_events, "edge_events_per_s": c.edge_events / wall,
                "pull_ms_total": c.pull_ms, "pull_launches": c.pull_launches,
                "pull_ms_avg": c.pull_ms / max(c.pull_launches, 1), "identical_to_first": same}
