@@ -10,6 +10,7 @@
 // so that a run can be reproduced.  The report is the reference's NS_LOG_INFO text.
 #include <cerrno>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -37,7 +38,7 @@ struct Options {
     bool handshake = false;            // NS-3 handshake window (GOSSIP_F_HANDSHAKE)
     bool hopBatch = false;             // hop-batched run (GOSSIP_F_HOP_BATCH)
     std::string mode = "auto";         // auto | csr | dense
-    std::string dumpLinks, dumpEvents, linksIn, eventsIn;
+    std::string dumpLinks, dumpEvents, linksIn, eventsIn, dumpTrace, netanim;
 };
 
 void usage() {
@@ -47,7 +48,7 @@ void usage() {
                  "                  [--seed=S] [--nodeSeed=S] [--topology=auto|exact|skip]\n"
                  "                  [--device=D] [--threads=T] [--maxWords=W] [--quiet]\n"
                  "                  [--noPeriodic] [--timing] [--handshake] [--hopBatch]\n                  [--mode=auto|csr|dense] [--dumpLinks=F] [--dumpEvents=F]\n"
-                 "                  [--links=F] [--events=F]\n");
+                 "                  [--links=F] [--events=F] [--dumpTrace=F] [--netanim=F]\n");
 }
 
 bool parse(int argc, char** argv, Options& o) {
@@ -106,12 +107,42 @@ bool parse(int argc, char** argv, Options& o) {
         else if (key == "dumpEvents") { if (!need()) return false; o.dumpEvents = val; }
         else if (key == "links") { if (!need()) return false; o.linksIn = val; }
         else if (key == "events") { if (!need()) return false; o.eventsIn = val; }
+        else if (key == "dumpTrace") { if (!need()) return false; o.dumpTrace = val; }
+        else if (key == "netanim") { if (!need()) return false; o.netanim = val; }
         else {
             std::fprintf(stderr, "unknown option --%s\n", key.c_str());
             return false;
         }
     }
     return true;
+}
+
+// SetupNetAnim (p2pnetwork.cc:153-190) as a NetAnim XML file: nodes on a ceil(sqrt(n)) grid
+// 100 units apart, "Node i" descriptions, colours by |peers| at the time SetupNetAnim runs --
+// Start() calls it before makeconnections, so every node still has 0 peers and is blue
+// (the reference's own behaviour) -- and one link per connection key.  The element layout
+// follows ns-3's AnimationInterface output; packet records (EnablePacketMetadata) are not
+// written.  Visual parity only: no NS-3 run is available to pin the format.
+bool write_netanim(const std::string& path, uint32_t n, const std::vector<uint32_t>& a,
+                   const std::vector<uint32_t>& b) {
+    FILE* f = std::fopen(path.c_str(), "w");
+    if (!f) return false;
+    const uint32_t grid = (uint32_t)std::ceil(std::sqrt((double)n));
+    const uint32_t rows = grid ? (n + grid - 1) / grid : 0;
+    std::fprintf(f, "<anim ver=\"netanim-3.108\" filetype=\"animation\" >\n");
+    std::fprintf(f, "<topology minX = \"0\" minY = \"0\" maxX = \"%u\" maxY = \"%u\">\n",
+                 grid ? 100u * (grid - 1) : 0u, rows ? 100u * (rows - 1) : 0u);
+    for (uint32_t i = 0; i < n; i++)
+        std::fprintf(f, "<node id=\"%u\" sysId=\"0\" locX=\"%u\" locY=\"%u\" />\n", i,
+                     100u * (i % grid), 100u * (i / grid));
+    for (uint32_t i = 0; i < n; i++) {
+        std::fprintf(f, "<nu p=\"c\" t=\"0\" id=\"%u\" r=\"0\" g=\"0\" b=\"255\" />\n", i);
+        std::fprintf(f, "<nu p=\"d\" t=\"0\" id=\"%u\" descr=\"Node %u\" />\n", i, i);
+    }
+    for (size_t k = 0; k < a.size(); k++)
+        std::fprintf(f, "<link fromId=\"%u\" toId=\"%u\" fd=\"\" td=\"\" ld=\"\" />\n", a[k], b[k]);
+    std::fprintf(f, "</topology>\n</anim>\n");
+    return std::fclose(f) == 0;
 }
 
 int die(const char* what) {
@@ -175,6 +206,12 @@ int main(int argc, char** argv) {
         for (size_t k = 0; f && k < a.size(); k++) std::fprintf(f, "%u %u\n", a[k], b[k]);
         if (f) std::fclose(f);
     }
+    if (!o.netanim.empty()) {
+        std::vector<uint32_t> a(gossip_topology_num_links(topo)), b(a.size());
+        gossip_topology_get_links(topo, a.data(), b.data());
+        if (!write_netanim(o.netanim, n, a, b)) { std::perror(o.netanim.c_str()); return 1; }
+        std::printf("NetAnim configured to save in %s\n", o.netanim.c_str());  // p2pnetwork.cc:189
+    }
     if (!o.dumpEvents.empty()) {
         std::vector<gossip_gen_event> ev(gossip_schedule_size(sched));
         gossip_schedule_get(sched, ev.data());
@@ -197,7 +234,7 @@ int main(int argc, char** argv) {
     else { usage(); return 2; }
     cfg.max_words = o.maxWords;
     cfg.flags = (o.timing ? GOSSIP_F_TIMING : 0u) | (o.handshake ? GOSSIP_F_HANDSHAKE : 0u) |
-                (o.hopBatch ? GOSSIP_F_HOP_BATCH : 0u);
+                (o.hopBatch ? GOSSIP_F_HOP_BATCH : 0u) | (o.dumpTrace.empty() ? 0u : GOSSIP_F_TRACE);
     gossip_engine* eng = nullptr;
     if (gossip_engine_create(&cfg, &eng)) return die("engine create");
     if (gossip_engine_set_topology(eng, topo)) return die("engine graph");
@@ -259,6 +296,19 @@ int main(int argc, char** argv) {
         std::fputs(buf.c_str(), stdout);
     }
     std::printf("All nodes stopped.\n");
+    if (!o.dumpTrace.empty()) {  // first contact per (node, shareId): tick, hop, via ReceiveShare
+        const uint64_t m = gossip_engine_trace_size(eng);
+        std::vector<uint32_t> tn(m), ti(m), th(m);
+        std::vector<int64_t> tt(m);
+        std::vector<uint8_t> tv(m);
+        if (m && gossip_engine_get_trace(eng, tn.data(), ti.data(), tt.data(), th.data(), tv.data()))
+            return die("trace");
+        FILE* f = std::fopen(o.dumpTrace.c_str(), "w");
+        if (!f) { std::perror(o.dumpTrace.c_str()); return 1; }
+        for (uint64_t k = 0; k < m; k++)
+            std::fprintf(f, "%u %u %lld %u %u\n", tn[k], ti[k], (long long)tt[k], th[k], (unsigned)tv[k]);
+        std::fclose(f);
+    }
     gossip_counters c{};
     gossip_engine_get_counters(eng, &c);
     std::fprintf(stderr,
