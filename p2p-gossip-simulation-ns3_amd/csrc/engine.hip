@@ -126,8 +126,18 @@ __device__ __forceinline__ uint64_t group_fix(uint64_t nw, uint64_t seen, uint64
 #include "pull_kernel.h"
 #include "dense_kernel.h"
 
+// Bitmaps above this size run k_pull<64,1> with non-temporal row accesses (pull_kernel.h).
+constexpr uint64_t kPullNtBytes = 16ull << 30;
+
 template <int LPW, int EPN>
 void launch_pull_t(uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
+    const bool nt = (uint64_t)a.n * a.stride * 8u > kPullNtBytes;
+    if constexpr (LPW == 64 && EPN == 1) {
+        if (nt) {
+            k_pull<64, 1, true><<<grid, 256, lds, s>>>(a);
+            return;
+        }
+    }
     if constexpr (LPW * EPN <= 64) k_pull<LPW, EPN><<<grid, 256, lds, s>>>(a);
 }
 

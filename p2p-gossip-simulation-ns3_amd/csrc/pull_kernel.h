@@ -56,6 +56,29 @@ constexpr int kInflight = PULL_INFLIGHT;  // peer-row loads in flight per lane
 // loads wait for the previous batch (profiles/r01/early_exit_ab.json).
 #define PULL_EARLY_EXIT 0
 #endif
+// Non-temporal row accesses: a template switch of k_pull<64,1>, chosen at launch by bitmap size
+// (engine.hip, kPullNtBytes).  On C4 (97 GB bitmaps) every row access non-temporal ran 128.6 ms
+// per launch against 132.1 ms; on C3 (2 GB bitmaps) 3.59 ms against 3.31 ms
+// (profiles/r01/nt_ab.json) -- so large windows stream, small ones keep the caches.
+template <bool NT>
+__device__ __forceinline__ ulonglong2 load_row16(const uint64_t* p) {
+    if constexpr (NT) {
+        const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+        return make_ulonglong2(__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1));
+    } else {
+        return *reinterpret_cast<const ulonglong2*>(p);
+    }
+}
+template <bool NT>
+__device__ __forceinline__ void store_row16(uint64_t* p, uint64_t x, uint64_t y) {
+    if constexpr (NT) {
+        unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+        __builtin_nontemporal_store((unsigned long long)x, q);
+        __builtin_nontemporal_store((unsigned long long)y, q + 1);
+    } else {
+        *reinterpret_cast<ulonglong2*>(p) = make_ulonglong2(x, y);
+    }
+}
 
 __host__ __device__ constexpr size_t pull_lds_bytes(uint32_t wact) {
     return (size_t)wact * 16u + (((size_t)wact + 15u) & ~(size_t)15u);
@@ -75,7 +98,7 @@ __device__ __forceinline__ uint32_t pull_cid_load(const PullArgs& a, uint32_t st
     return (c0 + idx < a.n && jj < end) ? (uint32_t)a.col[jj] : 0xffffffffu;
 }
 
-template <int LPW, int EPN>
+template <int LPW, int EPN, bool NT = false>
 __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
     constexpr int GRP = LPW * EPN;  // lanes per node
     constexpr int NPW = 64 / GRP;   // nodes per wave step
@@ -113,7 +136,7 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
             const uint64_t v = c0 + slot;
             const uint32_t lw = 2u * wl;
             if (v < n && lw < a.wact && (s_lp[lw] | s_lp[lw + 1u]) != 0ull)
-                s2c = *reinterpret_cast<const ulonglong2*>(a.seen + v * stride + a.wbase + lw);
+                s2c = load_row16<NT>(a.seen + v * stride + a.wbase + lw);
         }
         uint32_t cid0 = 0xffffffffu, cid1 = 0xffffffffu;
         unsigned long long nz0 = 0ull;
@@ -140,7 +163,7 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
                 const uint64_t v1 = c0 + step1 * NPW + slot;
                 const uint32_t lw1 = pass1 * 2u * LPW + 2u * wl;
                 if (v1 < n && lw1 < a.wact && (s_lp[lw1] | s_lp[lw1 + 1u]) != 0ull)
-                    s2n = *reinterpret_cast<const ulonglong2*>(a.seen + v1 * stride + a.wbase + lw1);
+                    s2n = load_row16<NT>(a.seen + v1 * stride + a.wbase + lw1);
             }
             uint32_t cid2 = 0xffffffffu;
             unsigned long long nz1 = 0ull;
@@ -248,7 +271,7 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
                             for (int t = 0; t < kInflight; t++) {
                                 q[t] = make_ulonglong2(0ull, 0ull);
                                 const bool issue = open && tneed && t0 + t < rem && ((z[t] >> (wl >> 3)) & 1u);
-                                if (issue) q[t] = *reinterpret_cast<const ulonglong2*>(Fw + (uint64_t)u[t] * stride);
+                                if (issue) q[t] = load_row16<NT>(Fw + (uint64_t)u[t] * stride);
                                 t_pe += wave_count(issue);
                             }
 #pragma unroll
@@ -323,12 +346,12 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
             if (own) {
                 uint64_t* sp = a.seen + (uint64_t)v * stride + w;
                 uint64_t* fp = a.Fnext + (uint64_t)v * stride + w;
-                if (ta) *reinterpret_cast<ulonglong2*>(fp) = make_ulonglong2(n0, n1);
+                if (ta) store_row16<NT>(fp, n0, n1);
                 if (swr) {
                     if (dead && !((f0 & f1) & WF_CLEAR))
                         sp[(f0 & WF_CLEAR) ? 0 : 1] = 0ull;
                     else
-                        *reinterpret_cast<ulonglong2*>(sp) = make_ulonglong2(s2.x | n0, s2.y | n1);
+                        store_row16<NT>(sp, s2.x | n0, s2.y | n1);
                 }
                 if (!dead) {
                     cnt += (uint32_t)(__popcll(n0) + __popcll(n1));
