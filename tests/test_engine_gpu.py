@@ -227,3 +227,25 @@ def test_large_sparse_invariants(gossip):
     assert int(st.gen.sum()) == len(ev)
     # a share born in the first ticks has flooded its component by tick 40
     assert int(st.recv.max()) > 0
+
+
+def test_parity_65536_sparse(gossip, oracle):
+    # SURVEY §7 minimum slice: a 65,536-node seeded case bit-exact, floods run to completion
+    # (the generations of the first tick after t_start; every id unique at this size).
+    n = 65536
+    topo = gossip.Topology.gnp(n, 16.0 / (n - 1), 61, gossip.TOPO_SKIP)
+    t_cut = gossip.seconds_to_ns(5.5)
+    ev = gossip.make_schedule(n, 62, T0, t_cut, t_gen_end_ns=T0 + L)
+    assert len(ev) > 10
+    eng = _engine_for(gossip, topo, ev, L, t_cut, flags=gossip.F_TRACE)
+    st = eng.stats()
+    a, b = topo.links()
+    r = oracle.run_replay(n, L, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=True)
+    for k in STATS:
+        assert np.array_equal(getattr(st, k), getattr(r, k)), k
+    node, sid, tick, hop, via = eng.trace()
+    tn, ti, tt, th, tv = r.trace
+    ek, ok = np.lexsort((sid, node)), np.lexsort((ti, tn))
+    assert np.array_equal(node[ek], tn[ok]) and np.array_equal(sid[ek], ti[ok])
+    assert np.array_equal(tick[ek], tt[ok] // L) and np.array_equal(hop[ek], th[ok])
+    assert int(st.recv.sum()) > n  # the floods covered the graph
