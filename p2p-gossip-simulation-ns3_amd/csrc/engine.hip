@@ -129,9 +129,19 @@ __device__ __forceinline__ uint64_t group_fix(uint64_t nw, uint64_t seen, uint64
 // Bitmaps above this size run k_pull<64,1> with non-temporal row accesses (pull_kernel.h).
 constexpr uint64_t kPullNtBytes = 16ull << 30;
 
+// GOSSIP_PULL_NT=0|1 overrides the size rule (A/B runs).
+int pull_nt_override() {
+    static const int v = [] {
+        const char* e = std::getenv("GOSSIP_PULL_NT");
+        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+    }();
+    return v;
+}
+
 template <int LPW, int EPN>
 void launch_pull_t(uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
-    const bool nt = (uint64_t)a.n * a.stride * 8u > kPullNtBytes;
+    const int ov = pull_nt_override();
+    const bool nt = ov >= 0 ? ov == 1 : (uint64_t)a.n * a.stride * 8u > kPullNtBytes;
     if constexpr (LPW == 64 && EPN == 1) {
         if (nt) {
             k_pull<64, 1, true><<<grid, 256, lds, s>>>(a);
