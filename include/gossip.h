@@ -173,6 +173,21 @@ int gossip_engine_set_schedule(gossip_engine* e, uint64_t num_events,
 int gossip_engine_set_schedule_obj(gossip_engine* e, const gossip_schedule* s);
 /* Stats snapshots at absolute times (PrintPeriodicStats, p2pnetwork.cc:201-204). */
 int gossip_engine_add_snapshot(gossip_engine* e, int64_t t_ns);
+/* NS-3 link timing: every hop of a share costs
+ *     latency + send_defer_ns + (len(message) + header_bytes) * ns_per_byte
+ * instead of the bare channel delay.  message = Share::ToString() (p2pnode.cc:6-11),
+ * "SHARE:<origin>:<shareId>:<timestamp>" with the timestamp streamed as a double in
+ * seconds (%g, 6 significant digits), so a share keeps one per-hop delay along its whole
+ * flood (a forwarded share is re-serialised from the parsed fields, p2pnode.cc:13-30,138).
+ * The 5 Mbps links of p2pnetwork.cc:113 give ns_per_byte = 1600; a data segment carries
+ * PPP(2) + IPv4(20) + TCP with the timestamp option (32) = 54 header bytes; TcpSocketBase
+ * defers SendPendingData by one TimeStep (send_defer_ns = 1).  Hop counts are unchanged
+ * (the delay is uniform along a flood); the PrintStatistics cut and the periodic snapshots
+ * see the later arrival times.  Needs GOSSIP_F_HOP_BATCH (hence unique share ids); call
+ * before gossip_engine_set_schedule.  gossip_share_message_length gives len(message). */
+int gossip_engine_set_link_timing(gossip_engine* e, int64_t ns_per_byte, uint32_t header_bytes,
+                                  int64_t send_defer_ns);
+uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t t_ns);
 /* First tick of the run window (floor(t_start/L)) and one past the last tick. */
 int64_t gossip_engine_first_tick(const gossip_engine* e);
 int64_t gossip_engine_end_tick(const gossip_engine* e);

@@ -33,6 +33,7 @@
 #include <memory>
 #include <queue>
 #include <random>
+#include <sstream>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -81,6 +82,7 @@ struct Share {
     uint32_t origin;
     uint32_t id;
     int64_t ts;
+    int64_t hop_ns;  // delivery delay of every Send of this share
 };
 
 struct Node {
@@ -129,6 +131,9 @@ struct oracle_sim {
     int64_t t_cut = 0;        // PrintStatistics time (simTime - 0.1)
     int64_t register_delay = 0;
     int64_t est_delay = 0;    // handshake model: connector sends before t_start+est are lost
+    bool link_timing = false; // serialisation model (oracle_set_link_timing)
+    int64_t link_npb = 0, link_defer = 0;
+    uint32_t link_hdr = 0;
     uint32_t id_mask = 0;
     std::vector<Node> nodes;
     std::vector<std::mt19937> rngs;  // p2pnode.h:34 (reference mode only)
@@ -192,7 +197,7 @@ struct oracle_sim {
             nd.sent++;
             nd.sent64++;
             edge_events++;
-            if (!lost) schedule(now + L, EV_ARRIVE, peer, share_idx, hop + 1);
+            if (!lost) schedule(now + shares[share_idx].hop_ns, EV_ARRIVE, peer, share_idx, hop + 1);
         }
     }
 
@@ -213,6 +218,14 @@ struct oracle_sim {
         sh.id = replay ? rp_id[e.arg] : unique_share_id(nd, e.t);
         nd.gen++;
         sh.ts = e.t;
+        sh.hop_ns = L;
+        if (link_timing) {
+            // Share::ToString (p2pnode.cc:6-11) with timestamp = Now().GetSeconds() (:119); a
+            // receiver re-serialises the parsed fields (:177,138), so every hop carries this string
+            std::ostringstream ss;
+            ss << "SHARE:" << sh.origin << ":" << sh.id << ":" << (double)e.t / 1e9;
+            sh.hop_ns += link_defer + ((int64_t)ss.str().size() + link_hdr) * link_npb;
+        }
         const bool was_seen = !nd.processed.insert(sh.id).second;
         shares.push_back(sh);
         gen_ns.push_back(e.t);
@@ -404,6 +417,18 @@ int oracle_set_handshake(oracle_sim* s, int64_t est_delay_ns, int64_t register_d
     if (s->events) return fail("set the handshake model before oracle_run");
     s->est_delay = est_delay_ns;
     s->register_delay = register_delay_ns;
+    return 0;
+}
+
+int oracle_set_link_timing(oracle_sim* s, int64_t ns_per_byte, uint32_t header_bytes,
+                           int64_t send_defer_ns) {
+    if (!s) return fail("null sim");
+    if (ns_per_byte < 0 || send_defer_ns < 0) return fail("negative link timing");
+    if (s->events) return fail("set link timing before oracle_run");
+    s->link_timing = true;
+    s->link_npb = ns_per_byte;
+    s->link_hdr = header_bytes;
+    s->link_defer = send_defer_ns;
     return 0;
 }
 

@@ -55,6 +55,16 @@ int oracle_create_replay(uint32_t num_nodes, int64_t latency_ns, int64_t t_start
  * oracle_run. */
 int oracle_set_handshake(oracle_sim* s, int64_t est_delay_ns, int64_t register_delay_ns);
 
+/* NS-3 link timing for either mode: a Send at time t is delivered at
+ *     t + latency + send_defer_ns + (len(Share::ToString()) + header_bytes) * ns_per_byte
+ * (TcpSocketBase's one-TimeStep SendPendingData deferral, then the PointToPoint device's
+ * serialisation at the link DataRate, then the channel delay).  5 Mbps links
+ * (p2pnetwork.cc:113): ns_per_byte = 1600, header_bytes = 54, send_defer_ns = 1.  Not
+ * modelled: device queueing behind other segments and ACKs, and the coalescing of the two
+ * sends to a duplicate peer into one segment.  Call before oracle_run. */
+int oracle_set_link_timing(oracle_sim* s, int64_t ns_per_byte, uint32_t header_bytes,
+                           int64_t send_defer_ns);
+
 /* Enable the per-(node, shareId) first-contact trace (small runs only). */
 int oracle_enable_trace(oracle_sim* s);
 

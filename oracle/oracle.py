@@ -39,6 +39,7 @@ def load():
                                              C.c_uint64, P, P, C.c_uint64, P, P, P, C.POINTER(P)]
         lib.oracle_enable_trace.argtypes = [P]
         lib.oracle_set_handshake.argtypes = [P, C.c_int64, C.c_int64]
+        lib.oracle_set_link_timing.argtypes = [P, C.c_int64, C.c_uint32, C.c_int64]
         lib.oracle_run.argtypes = [P]
         lib.oracle_get_stats.argtypes = [P] + [P] * 7
         lib.oracle_get_counters.argtypes = [P, P, P, P]
@@ -158,9 +159,22 @@ class OracleSim:
         self.close()
 
 
+# NS-3 5 Mbps point-to-point links (p2pnetwork.cc:113): ns per byte, PPP+IPv4+TCP(ts option)
+# header bytes, TcpSocketBase's one-TimeStep send deferral
+LINK_5MBPS = (1600, 54, 1)
+
+
+def _set_link_timing(s, link_timing):
+    if link_timing:
+        if load().oracle_set_link_timing(s._h, *(int(x) for x in link_timing)) != 0:
+            raise RuntimeError(load().oracle_last_error().decode())
+
+
 def run_reference(**kw) -> OracleResult:
     trace = kw.pop("trace", False)
+    link_timing = kw.pop("link_timing", None)
     s = OracleSim.reference(**kw)
+    _set_link_timing(s, link_timing)
     if trace:
         s.enable_trace()
     try:
@@ -169,9 +183,11 @@ def run_reference(**kw) -> OracleResult:
         s.close()
 
 
-def run_replay(*args, trace=False, handshake=None) -> OracleResult:
-    """handshake = (est_delay_ns, register_delay_ns): the NS-3 handshake-window model."""
+def run_replay(*args, trace=False, handshake=None, link_timing=None) -> OracleResult:
+    """handshake = (est_delay_ns, register_delay_ns): the NS-3 handshake-window model.
+    link_timing = (ns_per_byte, header_bytes, send_defer_ns), e.g. LINK_5MBPS."""
     s = OracleSim.replay(*args)
+    _set_link_timing(s, link_timing)
     if handshake:
         if load().oracle_set_handshake(s._h, int(handshake[0]), int(handshake[1])) != 0:
             raise RuntimeError(load().oracle_last_error().decode())

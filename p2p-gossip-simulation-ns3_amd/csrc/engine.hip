@@ -346,6 +346,12 @@ struct gossip_engine {
     bool batch = false, done = false;
     int64_t last_birth_tick = -1;
     std::vector<int64_t> ev_orig_ns;      // real generation time of ev[k]
+    // ---- NS-3 link timing (gossip_engine_set_link_timing; hop-batched runs only): share k
+    // reaches hop h at ev_orig_ns[k] + h * (L + ev_delta[k])
+    bool link_timing = false;
+    int64_t link_npb = 0, link_defer = 0;
+    uint32_t link_hdr = 0;
+    std::vector<int64_t> ev_delta;
     uint64_t* d_smask[4] = {};            // per ring slot: snapshot masks [snap][word]
     uint64_t* h_smask[4] = {};
     // ---- schedule (this shard)
@@ -980,8 +986,8 @@ int gossip_engine::tick_step(int64_t t) {
         WordCtl c = ctl[w];
         if (batch) {
             // column c (generation at real time tb, batched birth tick bt) is at hop t - bt: its
-            // arrival counts iff tb + hop*L < t_cut (PrintStatistics), and toward snapshot s
-            // iff tb + hop*L < T_s
+            // arrival counts iff tb + hop*L' < t_cut (PrintStatistics), and toward snapshot s
+            // iff tb + hop*L' < T_s, with L' = L (+ the share's serialisation, link timing)
             uint64_t km = 0ull;
             for (int bb = 0; bb < 64; bb++) {
                 const uint32_t q = col_src[(size_t)w * 64 + bb];
@@ -989,7 +995,8 @@ int gossip_engine::tick_step(int64_t t) {
                     km |= 1ull << bb;
                     continue;
                 }
-                const int64_t hop = t - ev[q].ns / L, ta = ev_orig_ns[q] + hop * L;
+                const int64_t hop = t - ev[q].ns / L;
+                const int64_t ta = ev_orig_ns[q] + hop * (L + (link_timing ? ev_delta[q] : 0));
                 if (ta < cfg.t_cut_ns) km |= 1ull << bb;
                 for (size_t s = 0; s < nsnap; s++)
                     if (hop >= 1 && ta < snaps[s].t_ns) {
@@ -1184,7 +1191,8 @@ int gossip_engine::decode_trace(int64_t t) {
                 const gossip_gen_event& e = ev[src];
                 const int64_t bt = e.ns / L;
                 const bool birth = (e.node == v && bt == t);
-                const int64_t real_t = batch ? ev_orig_ns[src] / L + (t - bt) : t;
+                const int64_t dl = link_timing ? ev_delta[src] : 0;
+                const int64_t real_t = batch ? (ev_orig_ns[src] + (t - bt) * (L + dl)) / L : t;
                 tr.push_back(Tr{v, e.share_id, real_t, (uint32_t)(t - bt), (uint8_t)(birth ? 0 : 1)});
             }
         }
@@ -1358,6 +1366,24 @@ int gossip_engine_add_snapshot(gossip_engine* e, int64_t t_ns) {
     return GOSSIP_OK;
 }
 
+int gossip_engine_set_link_timing(gossip_engine* e, int64_t ns_per_byte, uint32_t header_bytes,
+                                  int64_t send_defer_ns) {
+    if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    if (e->have_sched) return set_error(GOSSIP_ESTATE, "set link timing before the schedule");
+    if (!e->batch)
+        return set_error(GOSSIP_EINVAL, "link timing needs GOSSIP_F_HOP_BATCH (per-share cut masks)");
+    if (ns_per_byte < 0 || send_defer_ns < 0) return set_error(GOSSIP_EINVAL, "negative link timing");
+    // (any delay keeps hop order: it is the same at every hop of a share; the bound only
+    // keeps hop * (L + delay) far inside int64)
+    if (ns_per_byte > 1000000000ll || send_defer_ns > 1000000000ll)
+        return set_error(GOSSIP_EINVAL, "link timing above 1 s per byte / per send");
+    e->link_timing = true;
+    e->link_npb = ns_per_byte;
+    e->link_hdr = header_bytes;
+    e->link_defer = send_defer_ns;
+    return GOSSIP_OK;
+}
+
 int gossip_engine_set_schedule(gossip_engine* e, uint64_t num_events, const gossip_gen_event* ev) {
     if (!e || (num_events && !ev)) return set_error(GOSSIP_EINVAL, "NULL argument");
     if (!e->have_graph) return set_error(GOSSIP_ESTATE, "set the graph first");
@@ -1428,6 +1454,15 @@ int gossip_engine_set_schedule(gossip_engine* e, uint64_t num_events, const goss
             for (size_t k = 0; k < rm.size(); k++) {
                 e->ev[k] = rm[k].first;
                 e->ev_orig_ns[k] = rm[k].second;
+            }
+            if (e->link_timing) {
+                // per-share hop delay: the message is the same string at every hop
+                e->ev_delta.resize(rm.size());
+                for (size_t k = 0; k < rm.size(); k++) {
+                    const uint32_t len = gossip_share_message_length(e->ev[k].node, e->ev[k].share_id,
+                                                                     e->ev_orig_ns[k]);
+                    e->ev_delta[k] = e->link_defer + ((int64_t)len + e->link_hdr) * e->link_npb;
+                }
             }
             e->last_birth_tick = e->ev.empty() ? e->tick0 : e->ev.back().ns / e->L;
             e->cut_tick = -1;  // per-column cut instead

@@ -37,6 +37,7 @@ struct Options {
     bool timing = false;
     bool handshake = false;            // NS-3 handshake window (GOSSIP_F_HANDSHAKE)
     bool hopBatch = false;             // hop-batched run (GOSSIP_F_HOP_BATCH)
+    bool linkTiming = false;           // 5 Mbps serialisation per hop (implies --hopBatch)
     std::string mode = "auto";         // auto | csr | dense
     std::string dumpLinks, dumpEvents, linksIn, eventsIn, dumpTrace, netanim;
 };
@@ -47,7 +48,8 @@ void usage() {
                  "[--Latency=MS]\n"
                  "                  [--seed=S] [--nodeSeed=S] [--topology=auto|exact|skip]\n"
                  "                  [--device=D] [--threads=T] [--maxWords=W] [--quiet]\n"
-                 "                  [--noPeriodic] [--timing] [--handshake] [--hopBatch]\n                  [--mode=auto|csr|dense] [--dumpLinks=F] [--dumpEvents=F]\n"
+                 "                  [--noPeriodic] [--timing] [--handshake] [--hopBatch] [--linkTiming]\n"
+                 "                  [--mode=auto|csr|dense] [--dumpLinks=F] [--dumpEvents=F]\n"
                  "                  [--links=F] [--events=F] [--dumpTrace=F] [--netanim=F]\n");
 }
 
@@ -102,6 +104,7 @@ bool parse(int argc, char** argv, Options& o) {
         else if (key == "timing") o.timing = true;
         else if (key == "handshake") o.handshake = true;
         else if (key == "hopBatch") o.hopBatch = true;
+        else if (key == "linkTiming") o.linkTiming = o.hopBatch = true;
         else if (key == "mode") { if (!need()) return false; o.mode = val; }
         else if (key == "dumpLinks") { if (!need()) return false; o.dumpLinks = val; }
         else if (key == "dumpEvents") { if (!need()) return false; o.dumpEvents = val; }
@@ -238,6 +241,9 @@ int main(int argc, char** argv) {
     gossip_engine* eng = nullptr;
     if (gossip_engine_create(&cfg, &eng)) return die("engine create");
     if (gossip_engine_set_topology(eng, topo)) return die("engine graph");
+    // NS-3 link timing: 5 Mbps DataRate (p2pnetwork.cc:113) = 1600 ns/byte, 54 header bytes
+    // (PPP + IPv4 + TCP with timestamps), 1 ns TcpSocketBase send deferral (gossip.h)
+    if (o.linkTiming && gossip_engine_set_link_timing(eng, 1600, 54, 1)) return die("link timing");
     std::vector<double> per_t;
     if (o.periodic)
         for (double t = 10.0; t < o.simTime; t += 10.0) {  // Start(): p2pnetwork.cc:201-204

@@ -234,6 +234,16 @@ const char* gossip_last_error(void) { return g_last_error.c_str(); }
 const char* gossip_version(void) { return "gossip-mi355x 0.1.0"; }
 
 int64_t gossip_seconds_to_ns(double seconds) { return exact_scale_round(seconds, 1000000000ull); }
+
+// len(Share::ToString()) (p2pnode.cc:6-11): the same ostream formatting of the same fields.
+// timestamp = Simulator::Now().GetSeconds() (p2pnode.cc:119), taken here as ns / 1e9 in double
+// (ns-3 divides in int64x64 first: the two can differ by one ulp, which moves the 6-digit
+// rendering only on an exact decimal tie -- unpinned).
+uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t t_ns) {
+    std::ostringstream ss;
+    ss << "SHARE:" << origin << ":" << share_id << ":" << (double)t_ns / 1e9;
+    return (uint32_t)ss.str().size();
+}
 int64_t gossip_milliseconds_to_ns(double ms) { return exact_scale_round(ms, 1000000ull); }
 
 // ---------------------------------------------------------------------------------------

@@ -52,8 +52,13 @@ EXPORTED_SYMBOLS = (
     "gossip_engine_run", "gossip_engine_sync", "gossip_engine_get_stats",
     "gossip_engine_get_snapshot", "gossip_engine_get_counters", "gossip_engine_reset_timing",
     "gossip_engine_trace_size", "gossip_engine_get_trace", "gossip_engine_destroy",
-    "gossip_format_statistics", "gossip_format_periodic",
+    "gossip_format_statistics", "gossip_format_periodic", "gossip_engine_set_link_timing",
+    "gossip_share_message_length",
 )
+
+# NS-3 5 Mbps point-to-point links (p2pnetwork.cc:113): ns per byte, PPP+IPv4+TCP(timestamp
+# option) header bytes, TcpSocketBase's one-TimeStep send deferral (gossip.h)
+LINK_5MBPS = (1600, 54, 1)
 
 GEN_EVENT_DTYPE = np.dtype([("ns", "<i8"), ("node", "<u4"), ("share_id", "<u4")])
 
@@ -126,6 +131,8 @@ def load_library(path: str = LIB_PATH):
         "gossip_engine_set_schedule": (C.c_int, [P, u64, P]),
         "gossip_engine_set_schedule_obj": (C.c_int, [P, P]),
         "gossip_engine_add_snapshot": (C.c_int, [P, i64]),
+        "gossip_engine_set_link_timing": (C.c_int, [P, i64, u32, i64]),
+        "gossip_share_message_length": (u32, [u32, u32, i64]),
         "gossip_engine_first_tick": (i64, [P]),
         "gossip_engine_end_tick": (i64, [P]),
         "gossip_engine_current_tick": (i64, [P]),
@@ -156,6 +163,11 @@ def _check(rc: int, what: str):
 
 def _vp(a):
     return C.c_void_p(a.ctypes.data) if a is not None and a.size else None
+
+
+def share_message_length(origin: int, share_id: int, t_ns: int) -> int:
+    """len(Share::ToString()) of a share generated at t_ns (p2pnode.cc:6-11)."""
+    return int(load_library().gossip_share_message_length(int(origin), int(share_id), int(t_ns)))
 
 
 def seconds_to_ns(s: float) -> int:
@@ -296,6 +308,10 @@ class Engine:
     def add_snapshot(self, t_ns: int):
         _check(load_library().gossip_engine_add_snapshot(self._h, int(t_ns)), "snapshot")
 
+    def set_link_timing(self, ns_per_byte: int, header_bytes: int, send_defer_ns: int):
+        _check(load_library().gossip_engine_set_link_timing(
+            self._h, int(ns_per_byte), int(header_bytes), int(send_defer_ns)), "link timing")
+
     def set_schedule(self, ev: np.ndarray):
         ev = np.ascontiguousarray(ev, GEN_EVENT_DTYPE)
         _check(load_library().gossip_engine_set_schedule(self._h, ev.size, _vp(ev)), "set schedule")
@@ -396,7 +412,8 @@ class P2PGossipNetworkSimulation:
     """
 
     def __init__(self, numNodes: int, topo_seed: int = 1, node_seed: int = 1000, device: int = 0,
-                 topology_kind: int | None = None, threads: int = 8, flags: int = 0):
+                 topology_kind: int | None = None, threads: int = 8, flags: int = 0,
+                 link_timing=None):
         if numNodes < 2:
             # p2pnetwork.cc:82 calls nodes.Get(1) for the fix-up of row 0: out of range.
             raise GossipError("numNodes < 2: the reference's topology fix-up aborts")
@@ -407,6 +424,7 @@ class P2PGossipNetworkSimulation:
         self.kind = topology_kind
         self.threads = threads
         self.flags = flags
+        self.link_timing = link_timing  # e.g. LINK_5MBPS (needs flags |= F_HOP_BATCH)
         self.topology = None
         self.latency_ns = None
         self.engine = None
@@ -430,6 +448,8 @@ class P2PGossipNetworkSimulation:
         eng = Engine(self.numNodes, self.latency_ns, t_start, t_cut, device=self.device,
                      flags=self.flags)
         eng.set_topology(self.topology)
+        if self.link_timing:
+            eng.set_link_timing(*self.link_timing)
         times = []
         t = statsInterval
         while t < simulationTime:
