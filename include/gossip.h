@@ -243,6 +243,25 @@ int gossip_engine_get_trace(const gossip_engine* e, uint32_t* node, uint32_t* sh
 void gossip_engine_destroy(gossip_engine* e);
 
 /* ------------------------------------------------------------------------------------
+ * Event log: the reference's per-event NS_LOG_INFO lines (p2pnode.cc:88,122,143-144,160-161,
+ * 184,191-192) rendered from a first-contact trace (gossip_engine_get_trace, or ORACLE A's)
+ * plus the topology's peer lists, for events in [t_start, t_cut).  ev: the run's generation
+ * events with their real times, unique ids.  Lines of one nanosecond come in a canonical
+ * order (node, first contact before duplicates, share); with_time != 0 prefixes each line
+ * with "<t_ns>\t".  ns_per_byte/header_bytes/send_defer_ns: the link timing of the run
+ * (0, 0, 0 = ideal hop).  Writes into buf like gossip_format_statistics; returns the full
+ * length or a negative status.  Cost and size O(edge events): small runs only.
+ * ---------------------------------------------------------------------------------- */
+int64_t gossip_format_event_log(const gossip_topology* t, uint64_t num_events,
+                                const gossip_gen_event* ev, uint64_t num_trace,
+                                const uint32_t* tr_node, const uint32_t* tr_share_id,
+                                const uint32_t* tr_hop, const uint8_t* tr_via_recv,
+                                int64_t latency_ns, int64_t t_start_ns, int64_t t_cut_ns,
+                                int64_t ns_per_byte, uint32_t header_bytes,
+                                int64_t send_defer_ns, int with_time, char* buf,
+                                uint64_t buf_len);
+
+/* ------------------------------------------------------------------------------------
  * Report: the exact NS_LOG_INFO lines of PrintStatistics (p2pnetwork.cc:255-284) and
  * PrintPeriodicStats (:233-249), uint32 accumulators included.  Writes into buf
  * (NUL-terminated) and returns the full length; call with buf=NULL to size it.

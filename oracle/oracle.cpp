@@ -153,12 +153,24 @@ struct oracle_sim {
     std::vector<uint32_t> per_gen, per_proc, per_sock;
     bool trace = false;
     std::vector<TraceRec> tr;
+    bool log = false;
+    std::string lg;  // "<t_ns>\t<NS_LOG_INFO line>\n" in event order
     // snapshot at PrintStatistics
     bool have_stats = false;
     std::vector<uint32_t> s_gen, s_recv, s_fwd, s_proc, s_peers, s_sock;
     std::vector<uint64_t> s_sent;
     uint64_t edge_events = 0, events = 0;
     double wall = 0.0;
+
+    template <class F>
+    void log_line(int64_t t, F&& body) {
+        if (!log) return;
+        std::ostringstream os;
+        os << t << '\t';
+        body(os);
+        os << '\n';
+        lg += os.str();
+    }
 
     void schedule(int64_t t, uint32_t type, uint32_t node, uint32_t arg, uint32_t hop) {
         q.push(Event{t, seq++, type, node, arg, hop});
@@ -197,6 +209,11 @@ struct oracle_sim {
             nd.sent++;
             nd.sent64++;
             edge_events++;
+            const Share& sh = shares[share_idx];
+            log_line(now, [&](std::ostream& os) {  // :143-144
+                os << "Node " << nd.id << " sending share " << sh.origin << ":" << sh.id
+                   << " to peer " << peer;
+            });
             if (!lost) schedule(now + shares[share_idx].hop_ns, EV_ARRIVE, peer, share_idx, hop + 1);
         }
     }
@@ -209,6 +226,7 @@ struct oracle_sim {
     void on_gen(const Event& e) {
         Node& nd = nodes[e.node];
         if (nd.peers.empty()) {                  // :108-113
+            log_line(e.t, [&](std::ostream& os) { os << "Node " << nd.id << " has no peers to send shares to"; });
             if (!replay) schedule_next_share(nd, e.t);
             return;
         }
@@ -232,6 +250,7 @@ struct oracle_sim {
         gen_node.push_back(nd.id);
         gen_id.push_back(sh.id);
         if (!was_seen) record(nd.id, sh.id, e.t, 0, 0);
+        log_line(e.t, [&](std::ostream& os) { os << "Node " << nd.id << " generating new share " << sh.id; });  // :122
         gossip(nd, (uint32_t)(shares.size() - 1), e.t, 0);
         if (!replay) schedule_next_share(nd, e.t);
     }
@@ -240,11 +259,20 @@ struct oracle_sim {
     void on_arrive(const Event& e) {
         Node& nd = nodes[e.node];
         const Share& sh = shares[e.arg];
-        if (nd.processed.find(sh.id) != nd.processed.end()) return;  // :189-193 duplicate
+        if (nd.processed.find(sh.id) != nd.processed.end()) {         // :189-193 duplicate
+            log_line(e.t, [&](std::ostream& os) {
+                os << "Node " << nd.id << " already processed share " << sh.origin << ":" << sh.id;
+            });
+            return;
+        }
         nd.recv++;                                                   // ReceiveShare :157
         nd.processed.insert(sh.id);                                  // :158
         nd.fwd++;                                                    // :163
         record(nd.id, sh.id, e.t, e.hop, 1);
+        log_line(e.t, [&](std::ostream& os) {  // :160-161, timestamp streamed as a double
+            os << "Node " << nd.id << " received new share " << sh.origin << ":" << sh.id << ":"
+               << (double)sh.ts / 1e9 << " from origin " << sh.origin;
+        });
         gossip(nd, e.arg, e.t, e.hop);                               // :164
     }
 
@@ -253,6 +281,7 @@ struct oracle_sim {
         for (const auto& kv : links) {
             const uint32_t i = kv.first, j = kv.second;
             nodes[i].peersockets.insert(j);  // AddPeerSocket :144
+            log_line(e.t, [&](std::ostream& os) { os << "Node " << i << " added socket connection to peer " << j; });  // p2pnode.cc:88
             add_peer(nodes[i], j);           // AddPeer :145
             if (register_delay != 0) schedule(e.t + register_delay, EV_REGISTER, j, i, 0);
         }
@@ -264,10 +293,12 @@ struct oracle_sim {
                 const uint32_t i = kv.first, j = kv.second;
                 nodes[j].peersockets.insert(i);
                 nodes[j].peers.push_back(i);
+                log_line(e.t, [&](std::ostream& os) { os << "Node " << j << " received registration from peer " << i; });  // p2pnode.cc:184
             }
     }
 
     void on_register(const Event& e) {
+        log_line(e.t, [&](std::ostream& os) { os << "Node " << e.node << " received registration from peer " << e.arg; });
         nodes[e.node].peersockets.insert(e.arg);
         nodes[e.node].peers.push_back(e.arg);
     }
@@ -430,6 +461,22 @@ int oracle_set_link_timing(oracle_sim* s, int64_t ns_per_byte, uint32_t header_b
     s->link_hdr = header_bytes;
     s->link_defer = send_defer_ns;
     return 0;
+}
+
+int oracle_enable_log(oracle_sim* s) {
+    if (!s) return fail("null sim");
+    s->log = true;
+    return 0;
+}
+
+int64_t oracle_get_log(const oracle_sim* s, char* buf, uint64_t buf_len) {
+    if (!s) return fail("null sim");
+    if (buf && buf_len) {
+        const uint64_t k = std::min<uint64_t>(s->lg.size(), buf_len - 1);
+        std::memcpy(buf, s->lg.data(), k);
+        buf[k] = 0;
+    }
+    return (int64_t)s->lg.size();
 }
 
 int oracle_enable_trace(oracle_sim* s) {

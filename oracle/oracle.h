@@ -65,6 +65,12 @@ int oracle_set_handshake(oracle_sim* s, int64_t est_delay_ns, int64_t register_d
 int oracle_set_link_timing(oracle_sim* s, int64_t ns_per_byte, uint32_t header_bytes,
                            int64_t send_defer_ns);
 
+/* Record the NS_LOG_INFO lines of the gossip path (p2pnode.cc:88,110,122,143-144,160-161,
+ * 184,191-192) in event order, each as "<t_ns>\t<line>\n" (small runs only).
+ * oracle_get_log copies them into buf (NUL-terminated) and returns the full length. */
+int oracle_enable_log(oracle_sim* s);
+int64_t oracle_get_log(const oracle_sim* s, char* buf, uint64_t buf_len);
+
 /* Enable the per-(node, shareId) first-contact trace (small runs only). */
 int oracle_enable_trace(oracle_sim* s);
 

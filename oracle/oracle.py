@@ -38,6 +38,9 @@ def load():
         lib.oracle_create_replay.argtypes = [C.c_uint32, C.c_int64, C.c_int64, C.c_int64,
                                              C.c_uint64, P, P, C.c_uint64, P, P, P, C.POINTER(P)]
         lib.oracle_enable_trace.argtypes = [P]
+        lib.oracle_enable_log.argtypes = [P]
+        lib.oracle_get_log.argtypes = [P, C.c_char_p, C.c_uint64]
+        lib.oracle_get_log.restype = C.c_int64
         lib.oracle_set_handshake.argtypes = [P, C.c_int64, C.c_int64]
         lib.oracle_set_link_timing.argtypes = [P, C.c_int64, C.c_uint32, C.c_int64]
         lib.oracle_run.argtypes = [P]
@@ -81,6 +84,7 @@ class OracleResult:
     gen_events: tuple
     periodic: list
     trace: tuple | None
+    log: list | None = None  # [(t_ns, NS_LOG_INFO line)] in event order (log=True)
 
 
 class OracleSim:
@@ -117,6 +121,20 @@ class OracleSim:
 
     def enable_trace(self):
         load().oracle_enable_trace(self._h)
+
+    def enable_log(self):
+        load().oracle_enable_log(self._h)
+
+    def get_log(self):
+        lib = load()
+        k = lib.oracle_get_log(self._h, None, 0)
+        b = C.create_string_buffer(k + 1)
+        lib.oracle_get_log(self._h, b, k + 1)
+        out = []
+        for ln in b.value.decode().splitlines():
+            t, txt = ln.split("\t", 1)
+            out.append((int(t), txt))
+        return out
 
     def run(self, want_trace=False) -> OracleResult:
         lib = load()
@@ -170,20 +188,30 @@ def _set_link_timing(s, link_timing):
             raise RuntimeError(load().oracle_last_error().decode())
 
 
-def run_reference(**kw) -> OracleResult:
-    trace = kw.pop("trace", False)
-    link_timing = kw.pop("link_timing", None)
-    s = OracleSim.reference(**kw)
-    _set_link_timing(s, link_timing)
+def _run(s, trace, log):
     if trace:
         s.enable_trace()
+    if log:
+        s.enable_log()
     try:
-        return s.run(want_trace=trace)
+        r = s.run(want_trace=trace)
+        if log:
+            r.log = s.get_log()
+        return r
     finally:
         s.close()
 
 
-def run_replay(*args, trace=False, handshake=None, link_timing=None) -> OracleResult:
+def run_reference(**kw) -> OracleResult:
+    trace = kw.pop("trace", False)
+    log = kw.pop("log", False)
+    link_timing = kw.pop("link_timing", None)
+    s = OracleSim.reference(**kw)
+    _set_link_timing(s, link_timing)
+    return _run(s, trace, log)
+
+
+def run_replay(*args, trace=False, handshake=None, link_timing=None, log=False) -> OracleResult:
     """handshake = (est_delay_ns, register_delay_ns): the NS-3 handshake-window model.
     link_timing = (ns_per_byte, header_bytes, send_defer_ns), e.g. LINK_5MBPS."""
     s = OracleSim.replay(*args)
@@ -191,12 +219,7 @@ def run_replay(*args, trace=False, handshake=None, link_timing=None) -> OracleRe
     if handshake:
         if load().oracle_set_handshake(s._h, int(handshake[0]), int(handshake[1])) != 0:
             raise RuntimeError(load().oracle_last_error().decode())
-    if trace:
-        s.enable_trace()
-    try:
-        return s.run(want_trace=trace)
-    finally:
-        s.close()
+    return _run(s, trace, log)
 
 
 def seconds_to_ns(s):

@@ -40,6 +40,7 @@ struct Options {
     bool linkTiming = false;           // 5 Mbps serialisation per hop (implies --hopBatch)
     std::string mode = "auto";         // auto | csr | dense
     std::string dumpLinks, dumpEvents, linksIn, eventsIn, dumpTrace, netanim;
+    std::string log;  // per-event NS_LOG_INFO lines ("-" = stderr, where NS_LOG writes)
 };
 
 void usage() {
@@ -50,7 +51,8 @@ void usage() {
                  "                  [--device=D] [--threads=T] [--maxWords=W] [--quiet]\n"
                  "                  [--noPeriodic] [--timing] [--handshake] [--hopBatch] [--linkTiming]\n"
                  "                  [--mode=auto|csr|dense] [--dumpLinks=F] [--dumpEvents=F]\n"
-                 "                  [--links=F] [--events=F] [--dumpTrace=F] [--netanim=F]\n");
+                 "                  [--links=F] [--events=F] [--dumpTrace=F] [--netanim=F]\n"
+                 "                  [--log=F|-]\n");
 }
 
 bool parse(int argc, char** argv, Options& o) {
@@ -111,6 +113,7 @@ bool parse(int argc, char** argv, Options& o) {
         else if (key == "links") { if (!need()) return false; o.linksIn = val; }
         else if (key == "events") { if (!need()) return false; o.eventsIn = val; }
         else if (key == "dumpTrace") { if (!need()) return false; o.dumpTrace = val; }
+        else if (key == "log") { if (!need()) return false; o.log = val; }
         else if (key == "netanim") { if (!need()) return false; o.netanim = val; }
         else {
             std::fprintf(stderr, "unknown option --%s\n", key.c_str());
@@ -237,7 +240,11 @@ int main(int argc, char** argv) {
     else { usage(); return 2; }
     cfg.max_words = o.maxWords;
     cfg.flags = (o.timing ? GOSSIP_F_TIMING : 0u) | (o.handshake ? GOSSIP_F_HANDSHAKE : 0u) |
-                (o.hopBatch ? GOSSIP_F_HOP_BATCH : 0u) | (o.dumpTrace.empty() ? 0u : GOSSIP_F_TRACE);
+                (o.hopBatch ? GOSSIP_F_HOP_BATCH : 0u) | (o.dumpTrace.empty() && o.log.empty() ? 0u : GOSSIP_F_TRACE);
+    if (!o.log.empty() && o.handshake) {
+        std::fprintf(stderr, "gossip_sim: --log renders the ideal / --linkTiming models, not --handshake\n");
+        return 2;
+    }
     gossip_engine* eng = nullptr;
     if (gossip_engine_create(&cfg, &eng)) return die("engine create");
     if (gossip_engine_set_topology(eng, topo)) return die("engine graph");
@@ -302,13 +309,31 @@ int main(int argc, char** argv) {
         std::fputs(buf.c_str(), stdout);
     }
     std::printf("All nodes stopped.\n");
+    const uint64_t m_tr = o.dumpTrace.empty() && o.log.empty() ? 0 : gossip_engine_trace_size(eng);
+    std::vector<uint32_t> tn(m_tr), ti(m_tr), th(m_tr);
+    std::vector<int64_t> tt(m_tr);
+    std::vector<uint8_t> tv(m_tr);
+    if (m_tr && gossip_engine_get_trace(eng, tn.data(), ti.data(), tt.data(), th.data(), tv.data()))
+        return die("trace");
+    if (!o.log.empty()) {  // NS_LOG_INFO lines of the gossip path, rendered from the trace
+        std::vector<gossip_gen_event> ev(gossip_schedule_size(sched));
+        if (!ev.empty()) gossip_schedule_get(sched, ev.data());
+        const int64_t npb = o.linkTiming ? 1600 : 0, dfr = o.linkTiming ? 1 : 0;
+        const uint32_t hdr = o.linkTiming ? 54u : 0u;
+        const int64_t len = gossip_format_event_log(topo, ev.size(), ev.data(), m_tr, tn.data(), ti.data(),
+                                                    th.data(), tv.data(), L, t_start, t_cut, npb, hdr, dfr,
+                                                    0, nullptr, 0);
+        if (len < 0) return die("event log");
+        std::string buf((size_t)len + 1, '\0');
+        gossip_format_event_log(topo, ev.size(), ev.data(), m_tr, tn.data(), ti.data(), th.data(), tv.data(),
+                                L, t_start, t_cut, npb, hdr, dfr, 0, &buf[0], buf.size());
+        FILE* f = o.log == "-" ? stderr : std::fopen(o.log.c_str(), "w");
+        if (!f) { std::perror(o.log.c_str()); return 1; }
+        std::fwrite(buf.data(), 1, (size_t)len, f);
+        if (f != stderr) std::fclose(f);
+    }
     if (!o.dumpTrace.empty()) {  // first contact per (node, shareId): tick, hop, via ReceiveShare
-        const uint64_t m = gossip_engine_trace_size(eng);
-        std::vector<uint32_t> tn(m), ti(m), th(m);
-        std::vector<int64_t> tt(m);
-        std::vector<uint8_t> tv(m);
-        if (m && gossip_engine_get_trace(eng, tn.data(), ti.data(), tt.data(), th.data(), tv.data()))
-            return die("trace");
+        const uint64_t m = m_tr;
         FILE* f = std::fopen(o.dumpTrace.c_str(), "w");
         if (!f) { std::perror(o.dumpTrace.c_str()); return 1; }
         for (uint64_t k = 0; k < m; k++)

@@ -53,7 +53,7 @@ EXPORTED_SYMBOLS = (
     "gossip_engine_get_snapshot", "gossip_engine_get_counters", "gossip_engine_reset_timing",
     "gossip_engine_trace_size", "gossip_engine_get_trace", "gossip_engine_destroy",
     "gossip_format_statistics", "gossip_format_periodic", "gossip_engine_set_link_timing",
-    "gossip_share_message_length",
+    "gossip_share_message_length", "gossip_format_event_log",
 )
 
 # NS-3 5 Mbps point-to-point links (p2pnetwork.cc:113): ns per byte, PPP+IPv4+TCP(timestamp
@@ -133,6 +133,8 @@ def load_library(path: str = LIB_PATH):
         "gossip_engine_add_snapshot": (C.c_int, [P, i64]),
         "gossip_engine_set_link_timing": (C.c_int, [P, i64, u32, i64]),
         "gossip_share_message_length": (u32, [u32, u32, i64]),
+        "gossip_format_event_log": (i64, [P, u64, P, u64, P, P, P, P, i64, i64, i64, i64, u32,
+                                          i64, C.c_int, C.c_char_p, u64]),
         "gossip_engine_first_tick": (i64, [P]),
         "gossip_engine_end_tick": (i64, [P]),
         "gossip_engine_current_tick": (i64, [P]),
@@ -382,6 +384,35 @@ class Engine:
 
     def __del__(self):
         self.close()
+
+
+def format_event_log(topo: "Topology", ev: np.ndarray, trace, latency_ns: int, t_start_ns: int,
+                     t_cut_ns: int, link_timing=None, with_time: bool = True):
+    """The reference's NS_LOG_INFO gossip lines rendered from a first-contact trace
+    (gossip.h, gossip_format_event_log).  trace = (node, share_id, tick, hop, via) as returned by
+    Engine.trace(); ev = the run's generation events with real times.  Returns
+    [(t_ns, line)] when with_time, else the plain text."""
+    lib = load_library()
+    ev = np.ascontiguousarray(ev, GEN_EVENT_DTYPE)
+    node, sid, _tick, hop, via = (np.ascontiguousarray(x) for x in trace)
+    node, sid, hop = (np.ascontiguousarray(x, np.uint32) for x in (node, sid, hop))
+    via = np.ascontiguousarray(via, np.uint8)
+    npb, hdr, dfr = link_timing or (0, 0, 0)
+    args = [topo._h, ev.size, _vp(ev), node.size, _vp(node), _vp(sid), _vp(hop), _vp(via),
+            int(latency_ns), int(t_start_ns), int(t_cut_ns), int(npb), int(hdr), int(dfr),
+            1 if with_time else 0]
+    ln = lib.gossip_format_event_log(*args, None, 0)
+    _check(ln if ln < 0 else 0, "event log")
+    buf = C.create_string_buffer(ln + 1)
+    lib.gossip_format_event_log(*args, buf, ln + 1)
+    text = buf.value.decode()
+    if not with_time:
+        return text
+    out = []
+    for line in text.splitlines():
+        t, body = line.split("\t", 1)
+        out.append((int(t), body))
+    return out
 
 
 def format_statistics(st: Stats) -> str:
