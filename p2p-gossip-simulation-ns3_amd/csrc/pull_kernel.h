@@ -98,8 +98,16 @@ __device__ __forceinline__ uint32_t pull_cid_load(const PullArgs& a, uint32_t st
     return (c0 + idx < a.n && jj < end) ? (uint32_t)a.col[jj] : 0xffffffffu;
 }
 
+#ifndef PULL_WAVES_PER_EU
+#define PULL_WAVES_PER_EU 0  // A/B builds: cap VGPRs for more waves per SIMD (make variants)
+#endif
+#if PULL_WAVES_PER_EU
+#define PULL_OCC __attribute__((amdgpu_waves_per_eu(PULL_WAVES_PER_EU)))
+#else
+#define PULL_OCC
+#endif
 template <int LPW, int EPN, bool NT = false>
-__global__ __launch_bounds__(256) void k_pull(PullArgs a) {
+__global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     constexpr int GRP = LPW * EPN;  // lanes per node
     constexpr int NPW = 64 / GRP;   // nodes per wave step
     static_assert(GRP <= 64 && (64 % GRP) == 0, "lane layout");
