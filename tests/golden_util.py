@@ -1,4 +1,5 @@
 import glob
+import hashlib
 import json
 import os
 
@@ -17,3 +18,11 @@ def load(name):
     d = {k: z[k] for k in z.files}
     d["params"] = json.loads(str(d["params"]))
     return d
+
+
+def links_digest(a, b):
+    """SHA-256 over the uint32 key arrays: pins link sets too large to commit."""
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(a, np.uint32).tobytes())
+    h.update(np.ascontiguousarray(b, np.uint32).tobytes())
+    return h.hexdigest()

@@ -22,6 +22,10 @@ def test_product_topology_reproduces_golden_links(gossip, name):
     p = g["params"]
     t = gossip.Topology.gnp(p["num_nodes"], p["connection_prob"], p["topo_seed"], gossip.TOPO_EXACT)
     a, b = t.links()
-    assert np.array_equal(a, g["link_a"]) and np.array_equal(b, g["link_b"])
+    if "link_a" in g:
+        assert np.array_equal(a, g["link_a"]) and np.array_equal(b, g["link_b"])
+    else:
+        assert a.size == int(g["link_count"])
+        assert G.links_digest(a, b) == str(g["link_sha256"])
     peers, sockets = t.degrees()
     assert np.array_equal(peers, g["peers"]) and np.array_equal(sockets, g["sockets"])
