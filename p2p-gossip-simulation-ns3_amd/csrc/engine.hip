@@ -126,7 +126,7 @@ __device__ __forceinline__ uint64_t group_fix(uint64_t nw, uint64_t seen, uint64
 #include "pull_kernel.h"
 #include "dense_kernel.h"
 
-// Bitmaps above this size run k_pull<64,1> with non-temporal row accesses (pull_kernel.h).
+// Bitmaps above this size run k_pull<LPW,1> with non-temporal row accesses (pull_kernel.h).
 constexpr uint64_t kPullNtBytes = 16ull << 30;
 
 // GOSSIP_PULL_NT=0|1 overrides the size rule (A/B runs).
@@ -138,31 +138,31 @@ int pull_nt_override() {
     return v;
 }
 
-// A/B knob: GOSSIP_PULL_LPW=32|64 forces the word-lanes per node of the sparse pull.
+// A/B knob: GOSSIP_PULL_LPW=16|32|64 forces the word-lanes per node of the sparse pull.
 int pull_lpw_override() {
     static const int v = [] {
         const char* e = std::getenv("GOSSIP_PULL_LPW");
         const int x = e ? std::atoi(e) : 0;
-        return x == 32 || x == 64 ? x : 0;
+        return x == 16 || x == 32 || x == 64 ? x : 0;
     }();
     return v;
 }
 
-// Word-lanes per node for a launch of wact words on a sparse graph: a node's words are walked
-// in passes of 2*LPW words, so a window that ends in a partial pass leaves lanes idle for a
-// whole pass (C4 at 8 shards: 320 words = 2.5 passes of 128).  Take 32 lanes (passes of 64
-// words, two nodes per wave step) when that removes >= 10% of the lane slots.
-int pull_lanes_per_node(uint32_t wact) {
+// Word-lanes per node of the sparse pull for windows wider than 64 words.  32 lanes (passes of
+// 64 words, two nodes per wave step: twice the independent peer chains per wave, and a window
+// never ends in a half-idle 128-word pass) against 64 lanes, on the C4 / C3 benches
+// (profiles/r01/lanes_ab.json): C4 1216 words 127.7 -> 121.9 ms per launch, C4 8-shard 320 words
+// 44.0 -> 36.5 ms, C3 3.35 -> 3.06 ms; 16 lanes were slower on C4 (128.0 ms).
+int pull_lanes_per_node(uint32_t /*wact*/) {
     if (const int ov = pull_lpw_override()) return ov;
-    const uint64_t s64 = (wact + 127u) / 128u * 128u, s32 = (wact + 63u) / 64u * 64u;
-    return s32 * 10u <= s64 * 9u ? 32 : 64;
+    return 32;
 }
 
 template <int LPW, int EPN>
 void launch_pull_t(uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
     const int ov = pull_nt_override();
     const bool nt = ov >= 0 ? ov == 1 : (uint64_t)a.n * a.stride * 8u > kPullNtBytes;
-    if constexpr ((LPW == 64 || LPW == 32) && EPN == 1) {
+    if constexpr ((LPW == 64 || LPW == 32 || LPW == 16) && EPN == 1) {
         if (nt) {
             k_pull<LPW, 1, true><<<grid, 256, lds, s>>>(a);
             return;
@@ -1083,11 +1083,11 @@ int gossip_engine::tick_step(int64_t t) {
                 c.wact = std::min(kPullLdsWords, wact - wb);
                 int lpw = 8;
                 while (lpw < 64 && 2 * lpw < (int)c.wact) lpw *= 2;
-                // (a wide window on 32 lanes keeps one peer walk per node: the pipelined path)
-                const bool wide32 = lpw == 64 && split_edges && pull_lanes_per_node(c.wact) == 32;
-                if (wide32) lpw = 32;
+                // windows wider than 64 words keep one peer walk per node (the pipelined path)
+                const bool wide_window = lpw == 64 && split_edges;
+                if (wide_window) lpw = pull_lanes_per_node(c.wact);
                 int epn = 1;
-                while (split_edges && !wide32 && lpw * epn * 2 <= 64 && epn * 8 < avg_deg) epn *= 2;
+                while (split_edges && !wide_window && lpw * epn * 2 <= 64 && epn * 8 < avg_deg) epn *= 2;
                 // k_pull_wide (scalar peer loop) is opt-in: on C3 it measured 3.41 ms per launch
                 // against 3.33 ms for the lane-shuffle k_pull<64,1> (profiles/r01/ab_generic.json).
                 const bool wide = split_edges && n < (1u << 24) && !(cfg.flags & GOSSIP_F_GENERIC_PULL) &&

@@ -8,7 +8,9 @@
 //
 // Lane layout: a node is served by GRP = LPW x EPN lanes.  Word-lane wl owns the 16-B word pair
 // [2wl, 2wl+1] of every 2*LPW-word pass; edge-lane el takes every EPN-th peer.  Wide windows
-// (sparse graphs) use EPN = 1, LPW = 64: a wave reads 1 KiB of one peer row per instruction.
+// (sparse graphs) use EPN = 1, LPW = 32: a wave serves two nodes and reads 512 B of one peer
+// row of each per instruction (LPW = 64, one node and 1 KiB per instruction, measured 4-9 %
+// slower on C3/C4 and 20 % slower when a window ends in a half pass; engine.hip).
 // Narrow windows on dense graphs use EPN > 1: lanes split the peer list, then OR-reduce.
 // A launch covers the words [wbase, wbase + wact) of every row (wact <= kPullLdsWords).
 //
@@ -56,7 +58,7 @@ constexpr int kInflight = PULL_INFLIGHT;  // peer-row loads in flight per lane
 // loads wait for the previous batch (profiles/r01/early_exit_ab.json).
 #define PULL_EARLY_EXIT 0
 #endif
-// Non-temporal row accesses: a template switch of k_pull<64,1>, chosen at launch by bitmap size
+// Non-temporal row accesses: a template switch of k_pull<LPW,1>, chosen at launch by bitmap size
 // (engine.hip, kPullNtBytes).  On C4 (97 GB bitmaps) every row access non-temporal ran 128.6 ms
 // per launch against 132.1 ms; on C3 (2 GB bitmaps) 3.59 ms against 3.31 ms
 // (profiles/r01/nt_ab.json) -- so large windows stream, small ones keep the caches.
@@ -430,7 +432,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
 //   * a ballot compacts the peers that hold an occupied tile the node still needs, and the
 //     gather walks only those: per peer one v_readlane gives the id (a scalar row address,
 //     global_load with an SGPR base) and its tile byte (lanes of other tiles stay idle).
-// Same semantics, work skipping and pipeline as k_pull<64, 1>.
+// Same semantics, work skipping and pipeline as k_pull<LPW, 1>.
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t tiles_any(unsigned long long m) {
     // bit j = some lane of tile j (lanes 8j .. 8j+7) is set in the lane mask m
