@@ -138,6 +138,16 @@ int pull_nt_override() {
     return v;
 }
 
+// A/B knob: GOSSIP_DENSE_MIN_TILES = block tiles the K split aims for (default 512).
+uint64_t dense_min_tiles() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("GOSSIP_DENSE_MIN_TILES");
+        const long long x = e ? std::atoll(e) : 0;
+        return x > 0 ? (uint64_t)x : 512ull;
+    }();
+    return v;
+}
+
 // A/B knob: GOSSIP_PULL_LPW=16|32|64 forces the word-lanes per node of the sparse pull.
 int pull_lpw_override() {
     static const int v = [] {
@@ -1121,7 +1131,8 @@ int gossip_engine::tick_step(int64_t t) {
             gm.nt = wact / 4u;
             const uint32_t nst = n_pad / kStageK;
             uint32_t ks = 1;  // split K until the chip has ~2 tiles per CU (>= 2 stages per split)
-            while ((uint64_t)gm.mb * gm.nt * ks < 512 && ks * 4 <= nst) ks *= 2;
+            const uint64_t min_tiles = dense_min_tiles();
+            while ((uint64_t)gm.mb * gm.nt * ks < min_tiles && ks * 4 <= nst) ks *= 2;
             gm.ksplit = ks;
             gm.total = gm.mb * gm.nt * ks;
             k_dense_bits<<<(gm.total + 7u) / 8u * 8u, 512, 0, stream>>>(gm);
