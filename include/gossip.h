@@ -173,6 +173,23 @@ int gossip_engine_set_schedule(gossip_engine* e, uint64_t num_events,
 int gossip_engine_set_schedule_obj(gossip_engine* e, const gossip_schedule* s);
 /* Stats snapshots at absolute times (PrintPeriodicStats, p2pnetwork.cc:201-204). */
 int gossip_engine_add_snapshot(gossip_engine* e, int64_t t_ns);
+/* Row partition (the north star's multi-GPU layout): engine `rank` of `count`
+ * pulls, dedups and counts only its block of node rows (512-row blocks, rank r owns
+ * [r*B, min(n, (r+1)*B)) with B = roundup(ceil(n/count), 512)) and every rank holds the whole
+ * graph and frontier: after each tick the ranks exchange their rows of the new frontier, their
+ * tile-occupancy words and their liveness words.  Exchange backends: RCCL over xGMI
+ * (gossip_rccl_unique_id on one rank, shared out of band, then gossip_engine_connect_rccl on
+ * every rank; gossip_engine_run then exchanges on the engine's stream), or
+ * gossip_engine_group_run, which steps the engines of a partition in lockstep in one thread
+ * with device copies (one device: the rehearsal/test backend).  Per-node counters are non-zero
+ * only on the owning rank: sum them (and snapshot processed totals) over ranks; snapshot
+ * generation totals are global on every rank.  Call before the graph; not with
+ * GOSSIP_F_HANDSHAKE or share sharding. */
+int gossip_engine_set_row_partition(gossip_engine* e, uint32_t rank, uint32_t count);
+int gossip_rccl_unique_id(uint8_t* out, uint32_t len); /* len >= 128 (ncclUniqueId) */
+int gossip_engine_connect_rccl(gossip_engine* e, const uint8_t* unique_id, uint32_t len);
+int gossip_engine_group_run(gossip_engine** engines, uint32_t count, int64_t tick_end);
+
 /* NS-3 link timing: every hop of a share costs
  *     latency + send_defer_ns + (len(message) + header_bytes) * ns_per_byte
  * instead of the bare channel delay.  message = Share::ToString() (p2pnode.cc:6-11),

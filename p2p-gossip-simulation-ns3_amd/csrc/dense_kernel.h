@@ -43,6 +43,7 @@ struct BitsArgs {
     unsigned long long* acct;             // [5] += MAC ops x2 executed, [6] += tiles skipped
     uint32_t n, n_pad, kw, stride;
     uint32_t mb, nt, ksplit, total;  // row blocks, column tiles, K splits, mb*nt*ksplit
+    uint32_t mb0;                    // first row block (row partition)
 };
 
 constexpr uint32_t kDenseTile = 256;   // rows / columns per block tile
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(512, 1) void k_dense_bits(BitsArgs a) {
     if (T >= a.total) return;
     const uint32_t z = T % a.ksplit;
     const uint32_t nt = (T / a.ksplit) % a.nt;
-    const uint32_t mblk = T / (a.ksplit * a.nt);
+    const uint32_t mblk = a.mb0 + T / (a.ksplit * a.nt);
     const uint32_t t = threadIdx.x, lane = t & 63u, wid = t >> 6;
     const uint32_t wm = wid >> 2, wn = wid & 3u;
     const uint32_t w0 = nt * 4u;

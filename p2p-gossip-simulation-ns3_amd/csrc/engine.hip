@@ -23,6 +23,7 @@
 //               same-tick "own generation vs arrival" rule for id groups.
 //   k_reduce -- counter reductions for snapshots / totals.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -99,6 +100,7 @@ struct PullArgs {
     const unsigned long long* nz_cur;
     unsigned long long* nz_next;
     uint32_t ntw;
+    uint32_t v0 = 0;  // first node of this engine's row range (row partition; multiple of 64)
 };
 
 // Phase-ordered update of id groups inside one word (rare: only words holding groups).
@@ -380,6 +382,14 @@ struct gossip_engine {
     // reaches hop h at ev_orig_ns[k] + h * (L + ev_delta[k])
     bool link_timing = false;
     int64_t link_npb = 0, link_defer = 0;
+    // ---- row partition (gossip_engine_set_row_partition): this engine pulls, dedups and
+    // counts rows [v0, v1) only; the other rows of the frontier arrive by an exchange after
+    // every tick (RCCL over xGMI, or gossip_engine_group_run on one device)
+    uint32_t row_rank = 0, row_count = 1, v0 = 0, v1 = 0;
+    std::vector<uint32_t> row_lo;  // rank r owns [row_lo[r], row_lo[r + 1])
+    ncclComm_t comm = nullptr;
+    unsigned long long* d_live_all = nullptr;  // [row_count][live_all_cap] partial liveness
+    uint32_t live_all_cap = 0;
     uint32_t link_hdr = 0;
     std::vector<int64_t> ev_delta;
     uint64_t* d_smask[4] = {};            // per ring slot: snapshot masks [snap][word]
@@ -415,6 +425,7 @@ struct gossip_engine {
     struct Snap {
         int64_t t_ns, tick, r;
         uint64_t gen_total;
+        uint64_t own_gen_total;  // generations of this engine's rows (row partition)
     };
     std::vector<Snap> snaps;
     // ---- device state
@@ -471,6 +482,9 @@ struct gossip_engine {
     int prepare_instances();
     int compute_components();
     int tick_step(int64_t t);
+    int tick_step_a(int64_t t);  // up to the tick's kernels (pull, births, snapshot counts)
+    int tick_step_b(int64_t t);  // exchange (RCCL) + liveness read-back + bookkeeping
+    int exchange_rccl(int64_t t);
     int retire_from(int64_t known_tick, const unsigned long long* live);
     int alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t);
     int grow(uint32_t new_stride);
@@ -493,6 +507,8 @@ gossip_engine::~gossip_engine() {
     hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
+    hipFree(d_live_all);
+    if (comm) ncclCommDestroy(comm);
     for (int k = 0; k < kRing; k++) {
         hipFree(d_ctl[k]); hipFree(d_births[k]); hipFree(d_gphase[k]); hipFree(d_wflags[k]);
         hipHostFree(h_wflags[k]);
@@ -923,6 +939,11 @@ int gossip_engine::retire_from(int64_t known_tick, const unsigned long long* liv
 }
 
 int gossip_engine::tick_step(int64_t t) {
+    int rc = tick_step_a(t);
+    return rc ? rc : tick_step_b(t);
+}
+
+int gossip_engine::tick_step_a(int64_t t) {
     const int slot = (int)(t % kRing);
     // 1. liveness of tick t-kLag -> retire words whose floods have drained.
     {
@@ -999,7 +1020,7 @@ int gossip_engine::tick_step(int64_t t) {
                 b.kind = BIRTH_NORMAL;
             }
         }
-        B[nb++] = b;
+        if (e.node >= v0 && e.node < v1) B[nb++] = b;  // row partition: own nodes only
     }
     // 4. per-word control for this tick
     for (uint32_t w : reset_now) ctl[w].clear = ~0ull;
@@ -1077,7 +1098,8 @@ int gossip_engine::tick_step(int64_t t) {
         a.nz_cur = d_nz[fcur];
         a.nz_next = d_nz[nxt];
         a.ntw = ntw;
-        a.n = n; a.stride = stride; a.wbase = 0; a.wact = wact;
+        a.n = v1; a.stride = stride; a.wbase = 0; a.wact = wact;
+        a.v0 = v0;  // row partition: this engine's rows [v0, v1)
         a.noskip = (cfg.flags & GOSSIP_F_NOSKIP) ? 1u : 0u;
         const uint64_t chunks = ((uint64_t)n + 63) / 64;  // 64 nodes per wave step sequence
         const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, 2048));
@@ -1126,8 +1148,9 @@ int gossip_engine::tick_step(int64_t t) {
             // then consumed by k_pull (dedup/state/counters, untimed).
             BitsArgs gm;
             gm.Ab = d_Ab; gm.FT = d_FT; gm.inc = d_inc; gm.live_prev = a.live_prev; gm.acct = d_acct;
-            gm.n = n; gm.n_pad = n_pad; gm.kw = n_pad / 32u; gm.stride = stride;
-            gm.mb = n_pad / kDenseTile;
+            gm.n = v1; gm.n_pad = n_pad; gm.kw = n_pad / 32u; gm.stride = stride;
+            gm.mb0 = v0 / kDenseTile;  // row partition: this engine's row blocks only
+            gm.mb = (std::min(v1 + kDenseTile - 1u, n_pad) - v0) / kDenseTile;
             gm.nt = wact / 4u;
             const uint32_t nst = n_pad / kStageK;
             uint32_t ks = 1;  // split K until the chip has ~2 tiles per CU (>= 2 stages per split)
@@ -1167,13 +1190,75 @@ int gossip_engine::tick_step(int64_t t) {
         HIP_TRY(hipGetLastError());
     }
     if (smask_any) {  // hop-batched snapshots: arrivals of this tick that precede each snapshot
-        const uint64_t cells = (uint64_t)n * hw;
+        const uint64_t cells = (uint64_t)(v1 - v0) * hw;
         const uint32_t g = (uint32_t)std::min<uint64_t>((cells + 255) / 256, 4096);
         for (uint32_t s0 = 0; s0 < nsnap; s0 += kSnapGroup) {
-            k_snap_count<<<g, 256, 0, stream>>>(d_F[nxt], d_nz[nxt], stride, ntw, n, hw, d_smask[slot], s0,
+            k_snap_count<<<g, 256, 0, stream>>>(d_F[nxt] + (uint64_t)v0 * stride, d_nz[nxt] + (uint64_t)v0 * ntw,
+                                                stride, ntw, v1 - v0, hw, d_smask[slot], s0,
                                                 (uint32_t)std::min<size_t>(kSnapGroup, nsnap - s0), d_scalars);
             HIP_TRY(hipGetLastError());
         }
+    }
+    return GOSSIP_OK;
+}
+
+// Row partition over RCCL: every rank broadcasts its rows of F_next and of their tile
+// occupancy (an all-gather with per-rank block sizes) and all-gathers its partial liveness
+// words, which k_or_rows folds into the tick's global liveness.
+__global__ void k_or_rows(const unsigned long long* __restrict__ parts, uint32_t nparts, uint32_t cap,
+                          uint32_t wact, unsigned long long* __restrict__ live) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= wact) return;
+    unsigned long long x = 0ull;
+    for (uint32_t r = 0; r < nparts; r++) x |= parts[(uint64_t)r * cap + w];
+    live[w] = x;
+}
+
+#define NCCL_TRY(x)                                                                         \
+    do {                                                                                    \
+        ncclResult_t r_ = (x);                                                              \
+        if (r_ != ncclSuccess) return set_error(GOSSIP_EHIP, std::string("RCCL: ") + ncclGetErrorString(r_)); \
+    } while (0)
+
+int gossip_engine::exchange_rccl(int64_t t) {
+    const int nxt = fcur ^ 1, lv = (int)(t % 3);
+    const uint32_t wact = hw;
+    if (wact > live_all_cap) {
+        HIP_TRY(hipStreamSynchronize(stream));
+        hipFree(d_live_all);
+        d_live_all = nullptr;
+        live_all_cap = std::max(wact, stride);
+        HIP_TRY(hipMalloc(&d_live_all, (size_t)row_count * live_all_cap * 8));
+    }
+    NCCL_TRY(ncclGroupStart());
+    for (uint32_t r = 0; r < row_count; r++) {
+        const uint64_t lo = row_lo[r], hi = row_lo[r + 1];
+        if (hi <= lo) continue;
+        NCCL_TRY(ncclBroadcast(d_F[nxt] + lo * stride, d_F[nxt] + lo * stride, (hi - lo) * stride, ncclUint64,
+                               (int)r, comm, stream));
+        if (d_nz[nxt])
+            NCCL_TRY(ncclBroadcast(d_nz[nxt] + lo * ntw, d_nz[nxt] + lo * ntw, (hi - lo) * ntw, ncclUint64,
+                                   (int)r, comm, stream));
+    }
+    if (wact)
+        for (uint32_t r = 0; r < row_count; r++)  // all-gather into a [rank][cap] layout
+            NCCL_TRY(ncclBroadcast(d_live[lv], d_live_all + (uint64_t)r * live_all_cap, wact, ncclUint64,
+                                   (int)r, comm, stream));
+    NCCL_TRY(ncclGroupEnd());
+    if (wact) {
+        k_or_rows<<<(wact + 255) / 256, 256, 0, stream>>>(d_live_all, row_count, live_all_cap, wact, d_live[lv]);
+        HIP_TRY(hipGetLastError());
+    }
+    return GOSSIP_OK;
+}
+
+int gossip_engine::tick_step_b(int64_t t) {
+    const int lv = (int)(t % 3);
+    const uint32_t wact = hw;
+    const int nxt = fcur ^ 1;
+    if (comm) {
+        int rc = exchange_rccl(t);
+        if (rc) return rc;
     }
     // 6. liveness read-back (consumed kLag ticks later)
     {
@@ -1212,7 +1297,7 @@ int gossip_engine::decode_trace(int64_t t) {
         nz.resize((size_t)n * ntw);
         HIP_TRY(hipMemcpy(nz.data(), d_nz[fcur], nz.size() * 8, hipMemcpyDeviceToHost));
     }
-    for (uint32_t v = 0; v < n; v++)
+    for (uint32_t v = v0; v < v1; v++)
         for (uint32_t w = 0; w < hw; w++) {
             const uint32_t tl = w >> 4;
             if (!nz.empty() && !((nz[(size_t)v * ntw + (tl >> 6)] >> (tl & 63u)) & 1ull)) continue;  // stale row
@@ -1293,6 +1378,15 @@ int gossip_engine_set_graph(gossip_engine* e, uint32_t num_nodes, const int64_t*
     HIP_TRY(hipSetDevice(e->device));
     try {
         e->n = num_nodes;
+        // row partition: rank r owns [row_lo[r], row_lo[r+1]), blocks of 512 rows (dense tiles
+        // and 64-node pull waves both divide it)
+        e->row_lo.assign(e->row_count + 1, num_nodes);
+        const uint64_t rpr = ((uint64_t)(num_nodes + e->row_count - 1) / e->row_count + 511) / 512 * 512;
+        for (uint32_t r = 0; r < e->row_count; r++) e->row_lo[r] = (uint32_t)std::min<uint64_t>(num_nodes, r * rpr);
+        if (e->row_count > 1 && e->row_lo[e->row_count - 1] >= num_nodes)
+            return set_error(GOSSIP_EINVAL, "row partition: fewer than one 512-row block per rank");
+        e->v0 = e->row_lo[e->row_rank];
+        e->v1 = e->row_lo[e->row_rank + 1];
         e->nnz = (uint64_t)row_ptr[num_nodes];
         if (e->nnz >= (1ull << 31)) return set_error(GOSSIP_EINVAL, "more than 2^31 adjacency entries");
         e->h_rowptr.assign(row_ptr, row_ptr + num_nodes + 1);
@@ -1393,10 +1487,104 @@ int gossip_engine_set_topology(gossip_engine* e, const gossip_topology* t) {
 int gossip_engine_add_snapshot(gossip_engine* e, int64_t t_ns) {
     if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
     if (e->have_sched) return set_error(GOSSIP_ESTATE, "add snapshots before the schedule");
-    gossip_engine::Snap s{t_ns, t_ns / e->L, t_ns % e->L, 0};
+    gossip_engine::Snap s{t_ns, t_ns / e->L, t_ns % e->L, 0, 0};
     for (const auto& o : e->snaps)
         if (o.tick == s.tick) return set_error(GOSSIP_EINVAL, "two snapshots in one tick");
     e->snaps.push_back(s);
+    return GOSSIP_OK;
+}
+
+int gossip_engine_set_row_partition(gossip_engine* e, uint32_t rank, uint32_t count) {
+    if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    if (e->have_graph) return set_error(GOSSIP_ESTATE, "set the row partition before the graph");
+    if (count == 0 || rank >= count) return set_error(GOSSIP_EINVAL, "row partition: rank >= count");
+    if (e->handshake) return set_error(GOSSIP_EINVAL, "row partition: not with GOSSIP_F_HANDSHAKE");
+    if (e->cfg.shard_count > 1) return set_error(GOSSIP_EINVAL, "row partition: not with share sharding");
+    e->row_rank = rank;
+    e->row_count = count;
+    return GOSSIP_OK;
+}
+
+int gossip_rccl_unique_id(uint8_t* out, uint32_t len) {
+    if (!out || len < sizeof(ncclUniqueId)) return set_error(GOSSIP_EINVAL, "unique id buffer too small");
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    std::memcpy(out, &id, sizeof(id));
+    return GOSSIP_OK;
+}
+
+int gossip_engine_connect_rccl(gossip_engine* e, const uint8_t* id, uint32_t len) {
+    if (!e || !id || len < sizeof(ncclUniqueId)) return set_error(GOSSIP_EINVAL, "bad argument");
+    if (e->comm) return set_error(GOSSIP_ESTATE, "already connected");
+    HIP_TRY(hipSetDevice(e->device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    NCCL_TRY(ncclCommInitRank(&e->comm, (int)e->row_count, uid, (int)e->row_rank));
+    return GOSSIP_OK;
+}
+
+// One device (or peer-visible devices), one thread: the engines of one row partition step in
+// lockstep and exchange rows with device copies -- the rehearsal backend of the RCCL exchange.
+int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end) {
+    if (!es || count == 0) return set_error(GOSSIP_EINVAL, "NULL argument");
+    for (uint32_t r = 0; r < count; r++) {
+        gossip_engine* e = es[r];
+        if (!e || !e->have_sched) return set_error(GOSSIP_ESTATE, "set graph and schedule first");
+        if (e->row_count != count || e->row_rank != r) return set_error(GOSSIP_EINVAL, "engines must be ranks 0..count-1 of one partition");
+        if (e->comm) return set_error(GOSSIP_EINVAL, "group run is the non-RCCL backend");
+    }
+    gossip_engine* e0 = es[0];
+    if (tick_end > e0->tick_end) tick_end = e0->tick_end;
+    try {
+        std::vector<unsigned long long> acc, part;
+        while (e0->cur < tick_end) {
+            if (e0->batch && e0->cur > e0->last_birth_tick &&
+                std::find(e0->tile_alloc.begin(), e0->tile_alloc.end(), (uint8_t)1) == e0->tile_alloc.end()) {
+                for (uint32_t r = 0; r < count; r++) es[r]->done = true;
+                break;
+            }
+            const int64_t t = e0->cur;
+            for (uint32_t r = 0; r < count; r++) {
+                HIP_TRY(hipSetDevice(es[r]->device));
+                int rc = es[r]->tick_step_a(t);
+                if (rc) return rc;
+            }
+            for (uint32_t r = 0; r < count; r++) HIP_TRY(hipStreamSynchronize(es[r]->stream));
+            const int nxt = e0->fcur ^ 1, lv = (int)(t % 3);
+            const uint32_t wact = e0->hw, stride = e0->stride, ntw = e0->ntw;
+            for (uint32_t r = 1; r < count; r++)
+                if (es[r]->hw != wact || es[r]->stride != stride || es[r]->fcur != e0->fcur)
+                    return set_error(GOSSIP_EINVAL, "row partition engines diverged (different inputs?)");
+            for (uint32_t d = 0; d < count; d++)
+                for (uint32_t r = 0; r < count; r++) {
+                    const uint64_t lo = e0->row_lo[r], hi = e0->row_lo[r + 1];
+                    if (r == d || hi <= lo) continue;
+                    HIP_TRY(hipMemcpy(es[d]->d_F[nxt] + lo * stride, es[r]->d_F[nxt] + lo * stride,
+                                      (hi - lo) * stride * 8, hipMemcpyDeviceToDevice));
+                    if (es[d]->d_nz[nxt])
+                        HIP_TRY(hipMemcpy(es[d]->d_nz[nxt] + lo * ntw, es[r]->d_nz[nxt] + lo * ntw,
+                                          (hi - lo) * ntw * 8, hipMemcpyDeviceToDevice));
+                }
+            if (wact) {
+                acc.assign(wact, 0ull);
+                part.resize(wact);
+                for (uint32_t r = 0; r < count; r++) {
+                    HIP_TRY(hipMemcpy(part.data(), es[r]->d_live[lv], (size_t)wact * 8, hipMemcpyDeviceToHost));
+                    for (uint32_t w = 0; w < wact; w++) acc[w] |= part[w];
+                }
+                for (uint32_t r = 0; r < count; r++)
+                    HIP_TRY(hipMemcpy(es[r]->d_live[lv], acc.data(), (size_t)wact * 8, hipMemcpyHostToDevice));
+            }
+            for (uint32_t r = 0; r < count; r++) {
+                HIP_TRY(hipSetDevice(es[r]->device));
+                int rc = es[r]->tick_step_b(t);
+                if (rc) return rc;
+                es[r]->cur++;
+            }
+        }
+    } catch (const std::bad_alloc&) {
+        return set_error(GOSSIP_ENOMEM, "host allocation failed");
+    }
     return GOSSIP_OK;
 }
 
@@ -1505,10 +1693,14 @@ int gossip_engine_set_schedule(gossip_engine* e, uint64_t num_events, const goss
         int rc = e->prepare_instances();
         if (rc) return rc;
         for (auto& s : e->snaps) {
-            uint64_t g = 0;
+            uint64_t g = 0, own = 0;
             for (size_t k = 0; k < e->ev.size(); k++)
-                if ((e->batch ? e->ev_orig_ns[k] : e->ev[k].ns) < s.t_ns) g++;
+                if ((e->batch ? e->ev_orig_ns[k] : e->ev[k].ns) < s.t_ns) {
+                    g++;
+                    own += e->ev[k].node >= e->v0 && e->ev[k].node < e->v1;
+                }
             s.gen_total = g;
+            s.own_gen_total = own;
         }
         rc = e->alloc_device();
         if (rc) return rc;
@@ -1532,6 +1724,8 @@ int64_t gossip_engine_current_tick(const gossip_engine* e) { return e ? e->cur :
 int gossip_engine_run(gossip_engine* e, int64_t tick_end) {
     if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
     if (!e->have_sched) return set_error(GOSSIP_ESTATE, "set graph and schedule first");
+    if (e->row_count > 1 && !e->comm)
+        return set_error(GOSSIP_ESTATE, "row-partitioned engine: gossip_engine_connect_rccl or gossip_engine_group_run");
     HIP_TRY(hipSetDevice(e->device));
     if (tick_end > e->tick_end) tick_end = e->tick_end;
     try {
@@ -1609,7 +1803,7 @@ int gossip_engine_get_snapshot(gossip_engine* e, uint32_t k, int64_t* t_ns, uint
     unsigned long long v[2] = {0, 0};
     HIP_TRY(hipMemcpy(v, e->d_scalars + 2 + 2 * k, 16, hipMemcpyDeviceToHost));
     if (e->batch) {  // generations before T (all effective: unique ids) + arrivals before T
-        if (total_processed) *total_processed = s.gen_total + v[1];
+        if (total_processed) *total_processed = s.own_gen_total + v[1];
         return GOSSIP_OK;
     }
     if (total_processed) *total_processed = (s.tick <= e->tick0 && s.r == 0) ? 0 : (v[0] + v[1]);

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     unsigned long long nzacc = 0ull;
     const bool gather = a.inc == nullptr && EPN == 1;  // the pipelined id/occupancy loads
 
-    for (uint64_t c0 = wave * 64u; c0 < n; c0 += nwaves * 64u) {
+    for (uint64_t c0 = a.v0 + wave * 64u; c0 < n; c0 += nwaves * 64u) {
         const int64_t rp = a.rowptr[min(c0 + lane, n)];
         const int64_t rp_end = a.rowptr[min(c0 + 64u, n)];
         // item k = (step, pass): node c0 + step * NPW + slot, words wbase + pass * 2 LPW + 2 wl
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(256) void k_pull_wide(PullArgs a) {
         return (c0 + j < n && jj < end) ? (uint32_t)a.col[jj] : 0xffffffffu;
     };
 
-    for (uint64_t c0 = wave * 64u; c0 < n; c0 += nwaves * 64u) {
+    for (uint64_t c0 = a.v0 + wave * 64u; c0 < n; c0 += nwaves * 64u) {
         const int64_t rp = a.rowptr[min(c0 + lane, n)];
         const int64_t rp_end = a.rowptr[min(c0 + 64u, n)];
         uint32_t j = 0, pass = 0;  // item = (node c0 + j, pass)

@@ -53,7 +53,8 @@ EXPORTED_SYMBOLS = (
     "gossip_engine_get_snapshot", "gossip_engine_get_counters", "gossip_engine_reset_timing",
     "gossip_engine_trace_size", "gossip_engine_get_trace", "gossip_engine_destroy",
     "gossip_format_statistics", "gossip_format_periodic", "gossip_engine_set_link_timing",
-    "gossip_share_message_length", "gossip_format_event_log",
+    "gossip_share_message_length", "gossip_format_event_log", "gossip_engine_set_row_partition",
+    "gossip_rccl_unique_id", "gossip_engine_connect_rccl", "gossip_engine_group_run",
 )
 
 # NS-3 5 Mbps point-to-point links (p2pnetwork.cc:113): ns per byte, PPP+IPv4+TCP(timestamp
@@ -133,6 +134,10 @@ def load_library(path: str = LIB_PATH):
         "gossip_engine_add_snapshot": (C.c_int, [P, i64]),
         "gossip_engine_set_link_timing": (C.c_int, [P, i64, u32, i64]),
         "gossip_share_message_length": (u32, [u32, u32, i64]),
+        "gossip_engine_set_row_partition": (C.c_int, [P, u32, u32]),
+        "gossip_rccl_unique_id": (C.c_int, [C.c_char_p, u32]),
+        "gossip_engine_connect_rccl": (C.c_int, [P, C.c_char_p, u32]),
+        "gossip_engine_group_run": (C.c_int, [P, u32, i64]),
         "gossip_format_event_log": (i64, [P, u64, P, u64, P, P, P, P, i64, i64, i64, i64, u32,
                                           i64, C.c_int, C.c_char_p, u64]),
         "gossip_engine_first_tick": (i64, [P]),
@@ -165,6 +170,20 @@ def _check(rc: int, what: str):
 
 def _vp(a):
     return C.c_void_p(a.ctypes.data) if a is not None and a.size else None
+
+
+def rccl_unique_id() -> bytes:
+    """An RCCL communicator id (128 bytes) to share with every rank of a row partition."""
+    buf = C.create_string_buffer(128)
+    _check(load_library().gossip_rccl_unique_id(buf, 128), "rccl unique id")
+    return buf.raw
+
+
+def group_run(engines, tick_end: int | None = None):
+    """Step the engines of one row partition (ranks 0..count-1, one device) in lockstep."""
+    arr = (C.c_void_p * len(engines))(*[e._h.value if hasattr(e._h, "value") else e._h for e in engines])
+    end = engines[0].end_tick if tick_end is None else int(tick_end)
+    _check(load_library().gossip_engine_group_run(arr, len(engines), end), "group run")
 
 
 def share_message_length(origin: int, share_id: int, t_ns: int) -> int:
@@ -309,6 +328,15 @@ class Engine:
 
     def add_snapshot(self, t_ns: int):
         _check(load_library().gossip_engine_add_snapshot(self._h, int(t_ns)), "snapshot")
+
+    def set_row_partition(self, rank: int, count: int):
+        """Own node rows [rank block] only; exchange via connect_rccl or group_run (gossip.h)."""
+        _check(load_library().gossip_engine_set_row_partition(self._h, int(rank), int(count)),
+               "row partition")
+
+    def connect_rccl(self, unique_id: bytes):
+        _check(load_library().gossip_engine_connect_rccl(self._h, unique_id, len(unique_id)),
+               "rccl connect")
 
     def set_link_timing(self, ns_per_byte: int, header_bytes: int, send_defer_ns: int):
         _check(load_library().gossip_engine_set_link_timing(

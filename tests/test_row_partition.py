@@ -1,0 +1,107 @@
+"""Row partition: engine r of R pulls, dedups and counts only its block of node
+rows and the ranks exchange frontier rows, tile occupancy and liveness after every tick.  The
+lockstep one-device backend (gossip_engine_group_run) must give per-node counters that sum to
+the single engine's and to ORACLE A's bit for bit; the RCCL backend is exercised on one rank
+(ncclBroadcast / all-gather over a 1-rank communicator)."""
+import numpy as np
+import pytest
+
+from cases import L, T0
+
+pytestmark = pytest.mark.gpu
+
+SUM = ("gen", "recv", "fwd", "sent", "processed")
+
+
+def _inputs(gossip, n, p, seed, t_cut_s):
+    topo = gossip.Topology.gnp(n, p, seed, gossip.TOPO_EXACT)
+    t_cut = gossip.seconds_to_ns(t_cut_s)
+    ev = gossip.make_schedule(n, seed + 1, T0, t_cut)
+    return topo, t_cut, ev
+
+
+def _engine(gossip, n, t_cut, topo, ev, mode, flags, part=None, snaps=()):
+    e = gossip.Engine(n, L, T0, t_cut, mode=mode, flags=flags)
+    if part:
+        e.set_row_partition(*part)
+    e.set_topology(topo)
+    for t in snaps:
+        e.add_snapshot(t)
+    e.set_schedule(ev)
+    return e
+
+
+@pytest.mark.parametrize("mode,n,p,R,batch", [
+    ("csr", 1500, 0.01, 2, False),
+    ("csr", 1500, 0.01, 3, False),
+    ("dense", 1200, 0.3, 2, False),
+    ("csr", 1100, 0.02, 2, True),
+    ("dense", 1100, 0.3, 2, True),
+])
+def test_group_run_matches_single_engine_and_oracle(gossip, oracle, mode, n, p, R, batch):
+    topo, t_cut, ev = _inputs(gossip, n, p, 31, 7.3)
+    m = gossip.MODE_DENSE if mode == "dense" else gossip.MODE_CSR
+    flags = gossip.F_HOP_BATCH if batch else 0
+    snaps = [gossip.seconds_to_ns(6.0), gossip.seconds_to_ns(7.0)]
+    ref = _engine(gossip, n, t_cut, topo, ev, m, flags, snaps=snaps)
+    ref.run()
+    ref.sync()
+    want = ref.stats()
+    want_snap = [ref.snapshot(k) for k in range(len(snaps))]
+    ranks = [_engine(gossip, n, t_cut, topo, ev, m, flags, part=(r, R), snaps=snaps) for r in range(R)]
+    gossip.group_run(ranks)
+    for e in ranks:
+        e.sync()
+    got = [e.stats() for e in ranks]
+    for k in SUM:
+        total = sum(getattr(g, k).astype(np.uint64) for g in got)
+        assert np.array_equal(total, getattr(want, k).astype(np.uint64)), k
+    for k in ("peers", "sockets"):
+        assert np.array_equal(getattr(got[0], k), getattr(want, k)), k
+    # each rank counts only its own rows
+    owned = [np.nonzero(g.recv)[0] for g in got]
+    for r in range(R - 1):
+        assert owned[r].size == 0 or owned[r + 1].size == 0 or owned[r].max() < owned[r + 1].min()
+    for k, (t_ns, g_tot, p_tot) in enumerate(want_snap):
+        parts = [e.snapshot(k) for e in ranks]
+        assert all(x[0] == t_ns and x[1] == g_tot for x in parts)
+        assert sum(x[2] for x in parts) == p_tot
+    a, b = topo.links()
+    r = oracle.run_replay(n, L, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
+    for k in SUM:
+        assert np.array_equal(getattr(want, k), getattr(r, k)), k
+    for e in ranks + [ref]:
+        e.close()
+
+
+@pytest.mark.parametrize("mode,p", [("csr", 0.01), ("dense", 0.3)])
+def test_rccl_one_rank_matches_single_engine(gossip, mode, p):
+    n = 1000
+    topo, t_cut, ev = _inputs(gossip, n, p, 41, 7.0)
+    m = gossip.MODE_DENSE if mode == "dense" else gossip.MODE_CSR
+    ref = _engine(gossip, n, t_cut, topo, ev, m, 0)
+    ref.run()
+    ref.sync()
+    e = _engine(gossip, n, t_cut, topo, ev, m, 0, part=(0, 1))
+    e.connect_rccl(gossip.rccl_unique_id())
+    e.run()
+    e.sync()
+    a, b = ref.stats(), e.stats()
+    for k in SUM + ("peers", "sockets"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    e.close()
+    ref.close()
+
+
+def test_row_partition_needs_an_exchange(gossip):
+    n = 1100
+    topo, t_cut, ev = _inputs(gossip, n, 0.02, 51, 6.0)
+    e = _engine(gossip, n, t_cut, topo, ev, gossip.MODE_CSR, 0, part=(0, 2))
+    with pytest.raises(gossip.GossipError, match="connect_rccl or gossip_engine_group_run"):
+        e.run()
+    e.close()
+    e = gossip.Engine(400, L, T0, t_cut)  # blocks of 512 rows: rank 1 of 2 would own nothing
+    e.set_row_partition(1, 2)
+    with pytest.raises(gossip.GossipError, match="512-row block"):
+        e.set_topology(gossip.Topology.gnp(400, 0.02, 1, gossip.TOPO_EXACT))
+    e.close()
