@@ -1544,12 +1544,14 @@ int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end
                 break;
             }
             const int64_t t = e0->cur;
+            // ranks run one after another (each stands for its own GPU: its kernel times are
+            // then its own, not shared with the other ranks' concurrent kernels)
             for (uint32_t r = 0; r < count; r++) {
                 HIP_TRY(hipSetDevice(es[r]->device));
                 int rc = es[r]->tick_step_a(t);
                 if (rc) return rc;
+                HIP_TRY(hipStreamSynchronize(es[r]->stream));
             }
-            for (uint32_t r = 0; r < count; r++) HIP_TRY(hipStreamSynchronize(es[r]->stream));
             const int nxt = e0->fcur ^ 1, lv = (int)(t % 3);
             const uint32_t wact = e0->hw, stride = e0->stride, ntw = e0->ntw;
             for (uint32_t r = 1; r < count; r++)

@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--nodes", type=int, default=0)
     ap.add_argument("--modes", default="csr,dense")
     ap.add_argument("--batch", action="store_true", help="hop-batched run (GOSSIP_F_HOP_BATCH)")
+    ap.add_argument("--row-shards", type=int, default=0,
+                    help="rehearse an R-rank row partition on this GPU (gossip.group_run): reports "
+                         "the per-rank MFMA kernel time and the frontier exchange volume per tick")
     a = ap.parse_args()
     if a.config == "c2":
         n = a.nodes or 4096
@@ -66,6 +69,38 @@ def main():
         t_cut = T0 + 40 * L
         desc = (f"C5 slice: dense G(n,p) {n} nodes p=0.3, one flood batch of {a.width} concurrent "
                 f"shares at Philox-chosen origins, 1 GPU (setup {time.time() - t_setup:.0f} s)")
+    if a.row_shards > 1:
+        R = a.row_shards
+        engs = []
+        for r in range(R):
+            e = gossip.Engine(topo.num_nodes, L, T0, t_cut, mode=gossip.MODE_DENSE, flags=gossip.F_TIMING)
+            e.set_row_partition(r, R)
+            e.set_topology(topo)
+            e.set_schedule(ev)
+            e.reset_timing()
+            engs.append(e)
+        t0 = time.perf_counter()
+        gossip.group_run(engs)
+        for e in engs:
+            e.sync()
+        wall = time.perf_counter() - t0
+        cs = [e.counters() for e in engs]
+        ops = [c.dense_ops for c in cs]
+        ms = [c.pull_ms / max(c.pull_launches, 1) for c in cs]
+        util = [o / (c.pull_ms * 1e-3) / INT8_PEAK_OPS if c.pull_ms else None for o, c in zip(ops, cs)]
+        edge = sum(c.edge_events for c in cs)
+        n_ = topo.num_nodes
+        out = {"workload": desc, "mode": f"dense, row partition x{R} rehearsed on 1 GPU (group_run)",
+               "ticks": cs[0].ticks, "edge_events": edge,
+               "per_rank_mfma_ms_avg": ms, "per_rank_mfma_util": util,
+               "per_rank_mfma_ms_max": max(ms),
+               "projected_edge_events_per_s": edge / (cs[0].ticks * max(ms) * 1e-3),
+               "exchange_bytes_per_tick_per_rank": (n_ - n_ // R) * cs[0].words_hw * 8,
+               "group_wall_s_serialised": wall,
+               "note": "projection = per-tick time of the slowest rank's MFMA kernel; the exchange "
+                       "(all-gather of the frontier rows) and the dedup pull are not in it"}
+        print(json.dumps(out), flush=True)
+        return
     ref = None
     for mode in a.modes.split(","):
         m = gossip.MODE_DENSE if mode == "dense" else gossip.MODE_CSR
