@@ -150,6 +150,17 @@ uint64_t dense_min_tiles() {
     return v;
 }
 
+// A/B knob: GOSSIP_PULL_GRID = cap on the pull's blocks per launch (default 2048: 8,192 waves
+// striding over 64-node chunks).
+uint64_t pull_grid_cap() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("GOSSIP_PULL_GRID");
+        const long long x = e ? std::atoll(e) : 0;
+        return x > 0 ? (uint64_t)x : 2048ull;
+    }();
+    return v;
+}
+
 // A/B knob: GOSSIP_PULL_LPW=16|32|64 forces the word-lanes per node of the sparse pull.
 int pull_lpw_override() {
     static const int v = [] {
@@ -700,9 +711,24 @@ int gossip_engine::alloc_device() {
         words = (uint32_t)std::max<uint64_t>(w, 2);
     }
     stride = (words + kTileWords - 1) / kTileWords * kTileWords;  // rows start on 128-B lines
-    const uint64_t bm = (uint64_t)n * stride * 8;
     size_t freeb = 0, totalb = 0;
     HIP_TRY(hipMemGetInfo(&freeb, &totalb));
+    if (cfg.max_words == 0 && row_count == 1) {
+        // (row-partitioned ranks skip this: their strides must agree for the row exchange)
+        // Headroom over the estimate: up to +25% (at least 2 tiles) of row capacity, as far as
+        // device memory allows.  Unused capacity costs memory only -- the kernels touch the live
+        // words [0, wact) of a row -- while a short estimate on a graph whose bitmaps fill the
+        // card cannot be widened later (grow needs a fourth bitmap).  A C4 shard cut to a
+        // 20-tick slice measured 1,200 words estimated and more needed.
+        const uint64_t want = stride + std::max<uint64_t>(stride / 4, 2 * kTileWords);
+        const uint64_t other = (uint64_t)n * 24 + nnz * 4 + ((uint64_t)n + 1) * 8 +
+                               16ull * n * ((want + 1023u) / 1024u) + (2ull << 30);
+        const uint64_t per_word = 3ull * n * 8 + (dense ? 8ull * n_pad : 0ull);
+        uint64_t fit = freeb > other ? ((uint64_t)freeb - other) / per_word : 0ull;
+        fit = fit / kTileWords * kTileWords;
+        stride = (uint32_t)std::max<uint64_t>(stride, std::min<uint64_t>(want / kTileWords * kTileWords, fit));
+    }
+    const uint64_t bm = (uint64_t)n * stride * 8;
     const uint64_t need = 3 * bm + (uint64_t)n * 24 + (nnz * 4) + ((uint64_t)n + 1) * 8 +
                           (dense ? (uint64_t)stride * 8 * n_pad : 0ull);
     if (need > (uint64_t)freeb)
@@ -1102,7 +1128,7 @@ int gossip_engine::tick_step_a(int64_t t) {
         a.v0 = v0;  // row partition: this engine's rows [v0, v1)
         a.noskip = (cfg.flags & GOSSIP_F_NOSKIP) ? 1u : 0u;
         const uint64_t chunks = ((uint64_t)n + 63) / 64;  // 64 nodes per wave step sequence
-        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, 2048));
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, pull_grid_cap()));
         const double avg_deg = n ? (double)nnz / n : 0.0;
         // One launch per kPullLdsWords words of the window (its per-word state lives in LDS).
         // Lane layout: word-lanes cover the launch's words in one pass when possible (at least
