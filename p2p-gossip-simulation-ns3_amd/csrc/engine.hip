@@ -150,15 +150,18 @@ uint64_t dense_min_tiles() {
     return v;
 }
 
-// A/B knob: GOSSIP_PULL_GRID = cap on the pull's blocks per launch (default 2048: 8,192 waves
-// striding over 64-node chunks).
-uint64_t pull_grid_cap() {
-    static const uint64_t v = [] {
+// Cap on the pull's blocks per launch (4 waves each, striding over 64-node chunks).  Measured
+// (profiles/r01/grid_ab.jsonl, grid_ab2.jsonl): non-temporal (> 16 GiB) bitmaps like finer
+// work units -- C4 121.4 -> 119.5 ms per launch at 16,384 blocks, its 8-rank share 37.3 -> 36.3
+// ms -- while cache-resident ones keep 2,048 (C3 2.91 ms vs 3.06 ms at 16,384).
+// GOSSIP_PULL_GRID overrides (A/B runs).
+uint64_t pull_grid_cap(bool nt) {
+    static const long long ov = [] {
         const char* e = std::getenv("GOSSIP_PULL_GRID");
-        const long long x = e ? std::atoll(e) : 0;
-        return x > 0 ? (uint64_t)x : 2048ull;
+        return e ? std::atoll(e) : 0ll;
     }();
-    return v;
+    if (ov > 0) return (uint64_t)ov;
+    return nt ? 16384ull : 2048ull;
 }
 
 // A/B knob: GOSSIP_PULL_LPW=16|32|64 forces the word-lanes per node of the sparse pull.
@@ -1128,7 +1131,10 @@ int gossip_engine::tick_step_a(int64_t t) {
         a.v0 = v0;  // row partition: this engine's rows [v0, v1)
         a.noskip = (cfg.flags & GOSSIP_F_NOSKIP) ? 1u : 0u;
         const uint64_t chunks = ((uint64_t)n + 63) / 64;  // 64 nodes per wave step sequence
-        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, pull_grid_cap()));
+        const int nt_ov = pull_nt_override();
+        const bool nt_rows = nt_ov >= 0 ? nt_ov == 1 : (uint64_t)v1 * stride * 8u > kPullNtBytes;
+        const uint32_t grid =
+            (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, pull_grid_cap(nt_rows)));
         const double avg_deg = n ? (double)nnz / n : 0.0;
         // One launch per kPullLdsWords words of the window (its per-word state lives in LDS).
         // Lane layout: word-lanes cover the launch's words in one pass when possible (at least
