@@ -725,7 +725,7 @@ int gossip_engine::alloc_device() {
         // 20-tick slice measured 1,200 words estimated and more needed.
         const uint64_t want = stride + std::max<uint64_t>(stride / 4, 2 * kTileWords);
         const uint64_t other = (uint64_t)n * 24 + nnz * 4 + ((uint64_t)n + 1) * 8 +
-                               16ull * n * ((want + 1023u) / 1024u) + (2ull << 30);
+                               16ull * n * ((want + 1023u) / 1024u) + (4ull << 30);  // + RCCL / context
         const uint64_t per_word = 3ull * n * 8 + (dense ? 8ull * n_pad : 0ull);
         uint64_t fit = freeb > other ? ((uint64_t)freeb - other) / per_word : 0ull;
         fit = fit / kTileWords * kTileWords;
