@@ -38,6 +38,7 @@ sys.path.insert(0, os.path.join(ROOT, "p2p-gossip-simulation-ns3_amd"))
 import numpy as np  # noqa: E402
 
 import gossip  # noqa: E402
+import gossip.workloads as WL  # noqa: E402
 
 # BASELINE.json "metric", quoted on C4 (10M nodes)
 BASELINE_METRIC = "share-deliveries/sec (edge events) at 10M nodes, 1/2/4/8 GPUs; % HBM/MFMA peak"
@@ -48,29 +49,40 @@ L_NS = 5_000_000
 T_CUT_NS = 59_900_000_000
 
 WORKLOADS = {
-    # fit_shards: share shards one GPU's HBM must be cut into for the live window to fit
-    "C4": dict(nodes=10_000_000, fit_shards=2, topo_seed=4, node_seed=2000,
-               desc="C4: sparse G(n,p), 10M nodes, avg degree 16, 5 ms ticks"),
-    "C3": dict(nodes=1_000_000, fit_shards=1, topo_seed=3, node_seed=1000,
-               desc="C3: sparse G(n,p), 1M nodes, avg degree 16, 5 ms ticks"),
+    # fit_shards: share shards one GPU's HBM must be cut into for the live window to fit (the
+    # bench doubles it on its own when an engine reports GOSSIP_ECAPACITY / GOSSIP_ENOMEM)
+    "C4": dict(fit_shards=2, desc="C4: sparse G(n,p), 10M nodes, avg degree 16, 5 ms ticks"),
+    "C3": dict(fit_shards=1, desc="C3: sparse G(n,p), 1M nodes, avg degree 16, 5 ms ticks"),
 }
+CAPACITY_CODES = (-3, -5)  # GOSSIP_ENOMEM, GOSSIP_ECAPACITY
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(name, n_gpus):
-    """HBM bytes per pull launch from a committed rocprofv3 PMC pass of this bench command
-    (profiles/pmc_<workload>.json, written by tools/pmc_traffic.py), or None."""
+def pmc_traffic(name, line):
+    """HBM bytes per pull launch from the committed rocprofv3 PMC pass of this workload
+    (profiles/pmc_<workload>.json, written by tools/pmc_traffic.py), only when that pass ran the
+    same configuration as this line; otherwise (None, reason)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
-    if n_gpus != 1 or not os.path.exists(path):
-        return None
+    if line["n_gpus"] != 1:
+        return None, "PMC pass is single-GPU"
+    if not os.path.exists(path):
+        return None, f"no {os.path.relpath(path, ROOT)}"
     try:
         with open(path) as f:
-            return float(json.load(f)["hbm_bytes_per_launch"])
-    except Exception:
-        return None
+            d = json.load(f)
+    except Exception as e:  # a malformed file is reported, not fatal
+        return None, f"unreadable PMC file: {e}"
+    cfg = d.get("config") or {}
+    want = {"workload": name, "warmup": line["warmup"], "steps": line["steps"],
+            "live_words_per_node": line["config"]["live_words_per_node"],
+            "pull_variant": line["roofline"]["pull_variant"]}
+    diff = {k: (cfg.get(k), v) for k, v in want.items() if cfg.get(k) != v}
+    if diff:
+        return None, f"PMC pass config differs from this line: {diff}"
+    return float(d["hbm_bytes_per_launch"]), None
 
 
 def cpu_baseline(topo, ev, sample_shares, hops):
@@ -88,10 +100,63 @@ def cpu_baseline(topo, ev, sample_shares, hops):
     cut = f"cut after {hops} hops" if hops > 0 else "run to completion"
     return dict(value=r.edge_events / r.wall_s if r.wall_s > 0 else None, unit="edge events/s",
                 cores=1, kind="port",
-                sample=f"ORACLE A (event-driven P2PNode logic, unordered_set seen-sets) on the "
+                sample=f"ORACLE A (event-driven P2PNode logic, hash-set seen-sets) on the "
                        f"same graph, the first {len(sub)} generation(s) after t=10 s, floods "
                        f"{cut}: {r.edge_events} edge events in {r.wall_s:.2f} s of event loop "
                        f"(host nproc {os.cpu_count()}, threads=1)")
+
+
+def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, flags):
+    """Warm up and time every shard this rank owns; raises gossip.GossipError on failure."""
+    W, K = args.warmup, args.steps
+    slice_tick = SLICE_NS // L_NS
+    acc = dict(elapsed=0.0, edges=0, gens=0, launches=0, pull_ms=0.0, moved=0, dense=0, pe=0,
+               col=0, nz=0, srd=0, swr=0, fwr=0, words_hw=0, words_cap=0, dev_bytes=0, nt=0,
+               grid=0, ramp_ticks=0)
+    for s in my_shards:
+        t_eng = time.perf_counter()
+        eng = gossip.Engine(wl["nodes"], L_NS, T0_NS, T_CUT_NS, device=local, flags=flags,
+                            shard_rank=s, shard_count=shards)
+        try:
+            eng.set_topology(topo)
+            eng.set_schedule(ev)
+            # ramp: every tick from the first generation of the slice schedule (LIFE ticks before
+            # t = 10 s, plus the earlier floods of ids that recur in it) through W warm-up ticks
+            eng.run(slice_tick + W)
+            eng.sync()
+            c0 = eng.counters()
+            eng.reset_timing()
+            if dist:
+                dist.barrier()
+            eng.sync()
+            t0 = time.perf_counter()
+            eng.run(slice_tick + W + K)
+            eng.sync()
+            if dist:
+                dist.barrier()
+            t1 = time.perf_counter()
+            c1 = eng.counters()
+        finally:
+            eng.close()
+        acc["elapsed"] += t1 - t0
+        acc["edges"] += c1.edge_events - c0.edge_events
+        acc["gens"] += c1.generations
+        acc["pull_ms"] += c1.pull_ms
+        acc["launches"] += c1.pull_launches
+        for k, f in (("moved", "pull_bytes_moved"), ("dense", "pull_bytes"), ("pe", "pull_pair_edges"),
+                     ("col", "pull_col_ids"), ("nz", "pull_nz_reads"), ("srd", "pull_seen_reads"),
+                     ("swr", "pull_seen_writes"), ("fwr", "pull_f_writes")):
+            acc[k] += getattr(c1, f)
+        acc["words_hw"] = max(acc["words_hw"], c1.words_hw)
+        acc["words_cap"] = max(acc["words_cap"], c1.words_cap)
+        acc["dev_bytes"] = max(acc["dev_bytes"], c1.device_bytes)
+        acc["nt"], acc["grid"] = c1.pull_nt, c1.pull_grid
+        acc["ramp_ticks"] = c0.ticks
+        if rank == 0:
+            log(f"[bench] shard {s} of {shards}: {c1.edge_events - c0.edge_events} edge events in "
+                f"{(t1 - t0) * 1e3:.1f} ms, window {c1.words_hw} words, ramp {c0.ticks} ticks, "
+                f"engine setup + ramp {t0 - t_eng:.1f} s")
+    return acc
 
 
 def main():
@@ -116,7 +181,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    n_gpus = args.gpus
+    rehearsal = args.rehearse_shards > 1 and world == 1
+    if args.gpus != world and not rehearsal:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N > 1 with "
+                         f"torch.distributed.run (one process per GPU), or use --rehearse-shards")
+    n_gpus = world
     dist = None
     dev = None
     if world > 1:
@@ -132,98 +201,69 @@ def main():
         dist.init_process_group(backend)
         import gossip.dist as gd
     wl = dict(WORKLOADS[args.workload], name=args.workload)
+    wl["nodes"] = WL.CONFIGS[args.workload]["nodes"]
     if os.environ.get("GOSSIP_BENCH_NODES"):
         wl["nodes"] = int(os.environ["GOSSIP_BENCH_NODES"])
         wl["desc"] += f" [REHEARSAL: {wl['nodes']} nodes]"
     n = wl["nodes"]
-    p = 16.0 / (n - 1)
     W, K = args.warmup, args.steps
 
-    # Shards: at least what one GPU's HBM needs, at least one per rank, a multiple of the ranks.
-    passes = max(1, -(-wl["fit_shards"] // world))
-    shards = passes * world
-    my_shards = [rank * passes + q for q in range(passes)]
-    rehearsal = args.rehearse_shards > 1 and world == 1
-    if rehearsal:
-        shards, my_shards = args.rehearse_shards, [0]
-        wl["desc"] += f" [REHEARSAL: shard 0 of {shards} on one GPU]"
-    layout = (f"{shards} share shards, {len(my_shards)} per GPU in sequence" if len(my_shards) > 1
-              else f"{shards} share shards, one per GPU")
-
     t_setup = time.time()
-    topo = gossip.Topology.gnp(n, p, wl["topo_seed"], gossip.TOPO_SKIP, threads=args.threads)
-    # Steady-state slice: the share schedule is the reference's (node RNGs from t = 0, ids
-    # counted from t = 5 s); the slice starts at t = 10 s (tick 2000), where the U(2,5) s
-    # renewal density has settled at 1/3.5 s per node (at t = 5 s it is only 1/9 s).
+    topo = WL.topology(args.workload, nodes=n, threads=args.threads)
+    # Steady-state slice of the reference's continuous run: the schedule is the reference's
+    # (node RNGs from t = 0, ids counted from t = 5 s); the timed ticks start W ticks after
+    # t = 10 s (tick 2000).  The engine replays every generation of the LIFE ticks before 10 s
+    # and all earlier generations of the ids that occur in the slice (workloads.slice_schedule).
     t_gen_end = SLICE_NS + (W + K + 1) * L_NS
-    ev = gossip.make_schedule(n, wl["node_seed"], T0_NS, T_CUT_NS, t_gen_end_ns=t_gen_end,
-                              threads=args.threads)
-    ev = ev[ev["ns"] >= SLICE_NS]
+    ev, sinfo = WL.slice_schedule(n, WL.CONFIGS[args.workload]["node_seed"], SLICE_NS, t_gen_end,
+                                  threads=args.threads)
     flags = gossip.F_TIMING | (gossip.F_NOSKIP if args.noskip else 0)
     flags |= {"auto": 0, "wide": gossip.F_WIDE_PULL, "generic": gossip.F_GENERIC_PULL}[args.pull_kernel]
     if rank == 0:
         rp, _, _ = topo.csr()
         log(f"[bench] {wl['desc']}: {topo.num_nodes} nodes, {int(rp[-1])} directed entries, "
-            f"{len(ev)} generations in window, {layout}, setup {time.time() - t_setup:.1f} s")
+            f"{len(ev)} generations in the slice schedule ({sinfo['earlier_same_id']} earlier "
+            f"generations of recurring ids), setup {time.time() - t_setup:.1f} s")
 
-    elapsed = 0.0
-    edges = gens_done = launches = 0
-    pull_ms = 0.0
-    acc = dict(moved=0, dense=0, pe=0, col=0, nz=0, srd=0, swr=0, fwr=0)
-    words_hw = words_cap = dev_bytes = 0
-    tick0 = None
-    for s in my_shards:
-        t_eng = time.perf_counter()
-        eng = gossip.Engine(n, L_NS, SLICE_NS, T_CUT_NS, device=local, flags=flags,
-                            shard_rank=s, shard_count=shards)
-        eng.set_topology(topo)
-        eng.set_schedule(ev)
-        tick0 = eng.first_tick
-        eng.run(tick0 + W)
-        eng.sync()
-        c0 = eng.counters()
-        eng.reset_timing()
+    # Shards: at least what one GPU's HBM needs, at least one per rank, a multiple of the ranks;
+    # doubled (on every rank) when any rank's engine runs out of device memory.
+    passes = max(1, -(-wl["fit_shards"] // world))
+    while True:
+        shards = passes * world
+        my_shards = [rank * passes + q for q in range(passes)]
+        if rehearsal:
+            shards, my_shards = args.rehearse_shards * passes, [0]
+        err = None
+        try:
+            acc = run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, flags)
+        except gossip.GossipError as e:
+            if getattr(e, "code", None) not in CAPACITY_CODES:
+                raise
+            err = e
+        failed = 1.0 if err else 0.0
         if dist:
-            dist.barrier()
-        eng.sync()
-        t0 = time.perf_counter()
-        eng.run(tick0 + W + K)
-        eng.sync()
-        if dist:
-            dist.barrier()
-        t1 = time.perf_counter()
-        c1 = eng.counters()
-        elapsed += t1 - t0
-        edges += c1.edge_events - c0.edge_events
-        gens_done += c1.generations
-        pull_ms += c1.pull_ms
-        launches += c1.pull_launches
-        acc["moved"] += c1.pull_bytes_moved
-        acc["dense"] += c1.pull_bytes
-        acc["pe"] += c1.pull_pair_edges
-        acc["col"] += c1.pull_col_ids
-        acc["nz"] += c1.pull_nz_reads
-        acc["srd"] += c1.pull_seen_reads
-        acc["swr"] += c1.pull_seen_writes
-        acc["fwr"] += c1.pull_f_writes
-        words_hw = max(words_hw, c1.words_hw)
-        words_cap = max(words_cap, c1.words_cap)
-        dev_bytes = max(dev_bytes, c1.device_bytes)
-        eng.close()
+            failed = gd.allreduce_scalars([failed], op="max", device=dev)[0]
+        if not failed:
+            break
         if rank == 0:
-            log(f"[bench] shard {s} of {shards}: {c1.edge_events - c0.edge_events} edge events in "
-                f"{(t1 - t0) * 1e3:.1f} ms, window {c1.words_hw} words, engine setup + warm-up "
-                f"{t0 - t_eng:.1f} s")
+            log(f"[bench] {shards} shards do not fit ({err or 'another rank'}): retrying with {2 * shards}")
+        passes *= 2
+    layout = (f"{shards} share shards, {len(my_shards)} per GPU in sequence" if len(my_shards) > 1
+              else f"{shards} share shards, one per GPU")
+    if rehearsal:
+        wl["desc"] += f" [REHEARSAL: shard 0 of {shards} on one GPU]"
 
+    elapsed, edges, pull_ms = acc["elapsed"], acc["edges"], acc["pull_ms"]
+    launches = acc["launches"]
     if dist:
         elapsed, pull_ms_max = gd.allreduce_scalars([elapsed, pull_ms], op="max", device=dev)
-        edges_total, gens_total = gd.allreduce_scalars([edges, gens_done], op="sum", device=dev)
+        edges_total, gens_total = gd.allreduce_scalars([edges, acc["gens"]], op="sum", device=dev)
         edges_total = int(edges_total)
     else:
-        edges_total, gens_total, pull_ms_max = edges, gens_done, pull_ms
+        edges_total, gens_total, pull_ms_max = edges, acc["gens"], pull_ms
     if not rehearsal:
         # every counted generation of the simulated ticks ran on exactly one shard
-        want = int(np.count_nonzero(ev["ns"] < (tick0 + W + K) * L_NS))
+        want = int(np.count_nonzero(ev["ns"] < (SLICE_NS // L_NS + W + K) * L_NS))
         if int(gens_total) != want:
             raise SystemExit(f"shard coverage broken: {int(gens_total)} generations vs {want}")
 
@@ -236,6 +276,7 @@ def main():
         bytes_per_launch = per_launch(acc["moved"])
         dense_bytes_per_launch = per_launch(acc["dense"])  # SURVEY §8d dense formula
         achieved = bytes_per_launch / (avg_ms * 1e6) if avg_ms > 0 else 0.0  # GB/s
+        tick0 = SLICE_NS // L_NS
         out = {
             "metric": (BASELINE_METRIC if wl["name"] == "C4" and not rehearsal and "GOSSIP_BENCH_NODES" not in os.environ
                        else "share-deliveries/sec (edge events)"),
@@ -257,12 +298,14 @@ def main():
                 "avg_degree": 16,
                 "latency_ms": 5,
                 "ticks_timed": [tick0 + W, tick0 + W + K],
+                "ramp_ticks_before_timing": acc["ramp_ticks"],
+                "slice_schedule": sinfo,
                 "edge_events_timed": edges_total,
                 "share_shards": shards,
                 "shards_per_gpu": len(my_shards),
-                "live_words_per_node": words_hw,
-                "window_capacity_words": words_cap,
-                "device_gib": dev_bytes / 2**30,
+                "live_words_per_node": acc["words_hw"],
+                "window_capacity_words": acc["words_cap"],
+                "device_gib": acc["dev_bytes"] / 2**30,
                 "parallelism": f"share-shard x{shards} over {max(world, 1)} rank(s)",
             },
             "roofline": {
@@ -271,11 +314,18 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": pmc_traffic(wl["name"], n_gpus),
+                "traffic": None,
                 "kernel": "k_pull",
+                "pull_variant": {"nt_rows": acc["nt"], "grid": acc["grid"]},
                 "bytes_per_launch": bytes_per_launch,
+                "bytes_note": "algorithmic bytes of the occupancy-skipping pull: the peer-row, "
+                              "peer-id, occupancy, own-row and counter bytes it must move",
                 "dense_formula_bytes_per_launch": dense_bytes_per_launch,
-                "dense_formula_equiv_gbs": (dense_bytes_per_launch / (avg_ms * 1e6)) if avg_ms > 0 else None,
+                "dense_formula_frac": ((dense_bytes_per_launch / (avg_ms * 1e6)) / HBM_PEAK_GBS) if avg_ms > 0 else None,
+                "dense_formula_note": "SURVEY 8(d) B = 8(n+1)+4nnz+8Wq*nnz+24Wq*n+16n assumes every "
+                                      "peer-row word is read; the kernel skips dead, saturated and "
+                                      "unoccupied rows, so this ratio can exceed 1 and is not a "
+                                      "roofline fraction",
                 "avg_launch_ms": avg_ms,
                 "launches": launches,
                 "bytes_breakdown_per_launch": {
@@ -292,9 +342,14 @@ def main():
                 "pull_fraction_of_step": (pull_ms_max / (elapsed * 1e3)) if elapsed > 0 else None,
             },
         }
+        traffic, why = pmc_traffic(wl["name"], out)
+        out["roofline"]["traffic"] = traffic
+        if why:
+            out["roofline"]["traffic_note"] = why
         if n_gpus == 1 and world == 1 and not args.no_cpu_baseline:
             try:
-                out["cpu_baseline"] = cpu_baseline(topo, ev, args.cpu_sample, args.cpu_hops)
+                win = ev[ev["ns"] >= SLICE_NS]
+                out["cpu_baseline"] = cpu_baseline(topo, win, args.cpu_sample, args.cpu_hops)
             except Exception as e:  # the baseline is reported, never required
                 out["cpu_baseline"] = {"value": None, "error": str(e)}
         print(json.dumps(out), flush=True)

@@ -119,7 +119,7 @@ int gossip_shard_events(const gossip_topology* t, uint64_t num_events, const gos
  * ---------------------------------------------------------------------------------- */
 typedef struct gossip_engine gossip_engine;
 
-#define GOSSIP_MODE_AUTO 0
+#define GOSSIP_MODE_AUTO 0 /* DENSE when nnz >= 0.05 n^2 and 2048 <= n <= 2^19, else CSR */
 #define GOSSIP_MODE_CSR 1 /* bit-sliced frontier, CSR pull kernel              */
 #define GOSSIP_MODE_DENSE 2 /* adjacency x frontier as an int8 MFMA contraction (int32
                                accumulate: exact per-node copy counts); dense graphs,
@@ -205,6 +205,18 @@ int gossip_engine_group_run(gossip_engine** engines, uint32_t count, int64_t tic
 int gossip_engine_set_link_timing(gossip_engine* e, int64_t ns_per_byte, uint32_t header_bytes,
                                   int64_t send_defer_ns);
 uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t t_ns);
+/* Tuning options of one engine (results never depend on them; A/B runs and tests).  The
+ * environment variable in brackets gives the default:
+ *   "pull_nt"          -1 auto (non-temporal rows when the live frontier n x wact x 8 B exceeds
+ *                      16 GiB), 0 / 1 forced                              [GOSSIP_PULL_NT]
+ *   "pull_grid"        blocks per pull launch, 0 = auto (16,384 non-temporal, else 2,048)
+ *                                                                         [GOSSIP_PULL_GRID]
+ *   "pull_lpw"         word-lanes per node for windows > 64 words: 0 auto (32), 16, 32, 64
+ *                                                                         [GOSSIP_PULL_LPW]
+ *   "dense_min_tiles"  MFMA block tiles the K split aims for (512)  [GOSSIP_DENSE_MIN_TILES] */
+int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value);
+/* The mode the engine runs (AUTO resolves at gossip_engine_set_graph). */
+int gossip_engine_mode(const gossip_engine* e);
 /* First tick of the run window (floor(t_start/L)) and one past the last tick. */
 int64_t gossip_engine_first_tick(const gossip_engine* e);
 int64_t gossip_engine_end_tick(const gossip_engine* e);
@@ -246,6 +258,8 @@ typedef struct gossip_counters {
     uint64_t pull_seen_writes; /* own seen pairs written [16 B]                         */
     uint64_t pull_f_writes;    /* F_next pairs written [16 B]                           */
     uint64_t pull_nz_reads;    /* peer tile-occupancy words loaded [8 B]                */
+    uint32_t pull_nt;          /* variant of the last pull launch: 1 = non-temporal rows */
+    uint32_t pull_grid;        /* blocks of the last pull launch                        */
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 int gossip_engine_reset_timing(gossip_engine* e);

@@ -85,11 +85,79 @@ struct Share {
     int64_t hop_ns;  // delivery delay of every Send of this share
 };
 
+// Set of uint32 keys with the semantics of the reference's std::unordered_set<uint32_t>
+// processedShares / the key set of std::unordered_map<uint32_t, Ptr<Socket>> peersockets
+// (p2pnode.h:38-39): insert, find, size.  Open addressing in one allocation, so a 10M-node
+// replay (C4) builds and frees its 20M sets in seconds instead of minutes.
+class KeySet {
+  public:
+    // returns true if the key was not present
+    bool insert(uint32_t k) {
+        if (k == kEmpty) {
+            const bool fresh = !has_empty_key_;
+            has_empty_key_ = true;
+            size_ += fresh;
+            return fresh;
+        }
+        if ((used_ + 1) * 4 > slots_.size() * 3) rehash(slots_.empty() ? 8 : slots_.size() * 2);
+        size_t i = hash(k) & (slots_.size() - 1);
+        while (slots_[i] != kEmpty) {
+            if (slots_[i] == k) return false;
+            i = (i + 1) & (slots_.size() - 1);
+        }
+        slots_[i] = k;
+        used_++;
+        size_++;
+        return true;
+    }
+    bool contains(uint32_t k) const {
+        if (k == kEmpty) return has_empty_key_;
+        if (slots_.empty()) return false;
+        size_t i = hash(k) & (slots_.size() - 1);
+        while (slots_[i] != kEmpty) {
+            if (slots_[i] == k) return true;
+            i = (i + 1) & (slots_.size() - 1);
+        }
+        return false;
+    }
+    size_t size() const { return size_; }
+    void reserve(size_t k) {
+        size_t cap = 8;
+        while (cap * 3 < (k + 1) * 4) cap *= 2;
+        if (cap > slots_.size()) rehash(cap);
+    }
+    void clear() {
+        std::vector<uint32_t>().swap(slots_);
+        used_ = size_ = 0;
+        has_empty_key_ = false;
+    }
+
+  private:
+    static constexpr uint32_t kEmpty = 0xffffffffu;
+    static size_t hash(uint32_t k) { return (size_t)((k * 0x9E3779B1u) ^ (k >> 16)); }
+    void rehash(size_t cap) {
+        std::vector<uint32_t> old;
+        old.swap(slots_);
+        slots_.assign(cap, kEmpty);
+        used_ = 0;
+        for (uint32_t k : old)
+            if (k != kEmpty) {
+                size_t i = hash(k) & (cap - 1);
+                while (slots_[i] != kEmpty) i = (i + 1) & (cap - 1);
+                slots_[i] = k;
+                used_++;
+            }
+    }
+    std::vector<uint32_t> slots_;
+    size_t used_ = 0, size_ = 0;
+    bool has_empty_key_ = false;
+};
+
 struct Node {
     uint32_t id = 0;
     std::vector<uint32_t> peers;                  // p2pnode.h:32
-    std::unordered_set<uint32_t> peersockets;     // p2pnode.h:39 (keys only)
-    std::unordered_set<uint32_t> processed;       // p2pnode.h:38
+    KeySet peersockets;                           // p2pnode.h:39 (keys only)
+    KeySet processed;                             // p2pnode.h:38
     bool running = false;                         // p2pnode.h:36
     uint32_t sent = 0, recv = 0, gen = 0, fwd = 0;  // p2pnode.h:40-43
     uint64_t sent64 = 0;
@@ -205,7 +273,7 @@ struct oracle_sim {
     void gossip(Node& nd, uint32_t share_idx, int64_t now, uint32_t hop) {
         const bool lost = est_delay != 0 && now < t_start + est_delay;
         for (uint32_t peer : nd.peers) {
-            if (nd.peersockets.find(peer) == nd.peersockets.end()) continue;  // :131-135
+            if (!nd.peersockets.contains(peer)) continue;  // :131-135
             nd.sent++;
             nd.sent64++;
             edge_events++;
@@ -244,7 +312,7 @@ struct oracle_sim {
             ss << "SHARE:" << sh.origin << ":" << sh.id << ":" << (double)e.t / 1e9;
             sh.hop_ns += link_defer + ((int64_t)ss.str().size() + link_hdr) * link_npb;
         }
-        const bool was_seen = !nd.processed.insert(sh.id).second;
+        const bool was_seen = !nd.processed.insert(sh.id);
         shares.push_back(sh);
         gen_ns.push_back(e.t);
         gen_node.push_back(nd.id);
@@ -259,7 +327,7 @@ struct oracle_sim {
     void on_arrive(const Event& e) {
         Node& nd = nodes[e.node];
         const Share& sh = shares[e.arg];
-        if (nd.processed.find(sh.id) != nd.processed.end()) {         // :189-193 duplicate
+        if (nd.processed.contains(sh.id)) {                           // :189-193 duplicate
             log_line(e.t, [&](std::ostream& os) {
                 os << "Node " << nd.id << " already processed share " << sh.origin << ":" << sh.id;
             });
@@ -278,6 +346,17 @@ struct oracle_sim {
 
     // makeconnections (p2pnetwork.cc:99-107) -> ConnectPeerSockets (:133-150).
     void on_connect(const Event& e) {
+        {   // capacity only (a 10M-node replay): no effect on the sets' contents
+            std::vector<uint32_t> cnt(n, 0);
+            for (const auto& kv : links) {
+                cnt[kv.first]++;
+                cnt[kv.second]++;
+            }
+            for (uint32_t v = 0; v < n; v++) {
+                nodes[v].peers.reserve(cnt[v]);
+                nodes[v].peersockets.reserve(cnt[v]);
+            }
+        }
         for (const auto& kv : links) {
             const uint32_t i = kv.first, j = kv.second;
             nodes[i].peersockets.insert(j);  // AddPeerSocket :144

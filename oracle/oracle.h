@@ -109,6 +109,18 @@ int64_t oracle_milliseconds_to_ns(double ms);
 const char* oracle_last_error(void);
 void oracle_destroy(oracle_sim* s);
 
+/* ORACLE B (oracle_b.cpp): a bit-sliced, level-synchronous restatement of the same path for
+ * schedules whose share ids are all distinct (each share is then an independent flood; ideal
+ * hop).  Same link keys and counted-generation events as oracle_create_replay; arrivals count
+ * iff t + hop * latency < t_cut_ns.  Multi-threaded (num_threads); for sizes ORACLE A's event
+ * loop cannot reach.  Fails (-1, oracle_b_last_error) if two events share an id. */
+int oracle_b_run(uint32_t n, int64_t latency_ns, int64_t t_cut_ns, uint64_t num_links,
+                 const uint32_t* la, const uint32_t* lb, uint64_t num_events, const int64_t* ev_ns,
+                 const uint32_t* ev_node, const uint32_t* ev_id, int num_threads, uint32_t* gen,
+                 uint32_t* recv, uint32_t* fwd, uint64_t* sent, uint32_t* processed,
+                 uint32_t* peers, uint32_t* sockets, uint64_t* edge_events);
+const char* oracle_b_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,9 @@ def load():
         lib.oracle_milliseconds_to_ns.restype = C.c_int64
         lib.oracle_last_error.restype = C.c_char_p
         lib.oracle_destroy.argtypes = [P]
+        lib.oracle_b_run.argtypes = [C.c_uint32, C.c_int64, C.c_int64, C.c_uint64, P, P, C.c_uint64,
+                                     P, P, P, C.c_int] + [P] * 8
+        lib.oracle_b_last_error.restype = C.c_char_p
         _lib = lib
     return _lib
 
@@ -220,6 +223,30 @@ def run_replay(*args, trace=False, handshake=None, link_timing=None, log=False) 
         if load().oracle_set_handshake(s._h, int(handshake[0]), int(handshake[1])) != 0:
             raise RuntimeError(load().oracle_last_error().decode())
     return _run(s, trace, log)
+
+
+def run_oracle_b(num_nodes, latency_ns, t_cut_ns, link_a, link_b, ev_ns, ev_node, ev_id,
+                 threads=8) -> OracleResult:
+    """ORACLE B (oracle_b.cpp): bit-sliced level-synchronous restatement for schedules with
+    distinct share ids; same inputs as run_replay (t_start is implicit: every edge is up before
+    the first counted generation).  Stats only (no trace / periodic)."""
+    lib = load()
+    n = int(num_nodes)
+    a = np.ascontiguousarray(link_a, np.uint32)
+    b = np.ascontiguousarray(link_b, np.uint32)
+    ns = np.ascontiguousarray(ev_ns, np.int64)
+    nd = np.ascontiguousarray(ev_node, np.uint32)
+    ids = np.ascontiguousarray(ev_id, np.uint32)
+    u = [np.empty(n, np.uint32) for _ in range(6)]
+    sent = np.empty(n, np.uint64)
+    ee = C.c_uint64()
+    rc = lib.oracle_b_run(n, int(latency_ns), int(t_cut_ns), a.size, _vp(a), _vp(b), ns.size,
+                          _vp(ns), _vp(nd), _vp(ids), int(threads), _vp(u[0]), _vp(u[1]),
+                          _vp(u[2]), _vp(sent), _vp(u[3]), _vp(u[4]), _vp(u[5]), C.byref(ee))
+    if rc != 0:
+        raise RuntimeError(lib.oracle_b_last_error().decode())
+    return OracleResult(u[0], u[1], u[2], sent, u[3], u[4], u[5], ee.value, 0, 0.0, (a, b),
+                        (ns, nd, ids), [], None)
 
 
 def seconds_to_ns(s):

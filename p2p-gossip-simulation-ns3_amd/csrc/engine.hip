@@ -129,49 +129,24 @@ __device__ __forceinline__ uint64_t group_fix(uint64_t nw, uint64_t seen, uint64
 #include "dense_kernel.h"
 
 // Bitmaps above this size run k_pull<LPW,1> with non-temporal row accesses (pull_kernel.h).
+// The size is the launch's LIVE footprint, n x wact words (not the allocated capacity, which
+// depends on how much headroom the device had free at allocation time).
 constexpr uint64_t kPullNtBytes = 16ull << 30;
 
-// GOSSIP_PULL_NT=0|1 overrides the size rule (A/B runs).
-int pull_nt_override() {
-    static const int v = [] {
-        const char* e = std::getenv("GOSSIP_PULL_NT");
-        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
-    }();
-    return v;
-}
-
-// A/B knob: GOSSIP_DENSE_MIN_TILES = block tiles the K split aims for (default 512).
-uint64_t dense_min_tiles() {
-    static const uint64_t v = [] {
-        const char* e = std::getenv("GOSSIP_DENSE_MIN_TILES");
-        const long long x = e ? std::atoll(e) : 0;
-        return x > 0 ? (uint64_t)x : 512ull;
-    }();
-    return v;
+// Environment defaults of the per-engine tuning options (gossip_engine_set_option overrides
+// them per engine; A/B runs and tests).
+int64_t env_option(const char* name, int64_t dflt) {
+    const char* e = std::getenv(name);
+    return e && *e ? (int64_t)std::atoll(e) : dflt;
 }
 
 // Cap on the pull's blocks per launch (4 waves each, striding over 64-node chunks).  Measured
 // (profiles/r01/grid_ab.jsonl, grid_ab2.jsonl): non-temporal (> 16 GiB) bitmaps like finer
 // work units -- C4 121.4 -> 119.5 ms per launch at 16,384 blocks, its 8-rank share 37.3 -> 36.3
 // ms -- while cache-resident ones keep 2,048 (C3 2.91 ms vs 3.06 ms at 16,384).
-// GOSSIP_PULL_GRID overrides (A/B runs).
-uint64_t pull_grid_cap(bool nt) {
-    static const long long ov = [] {
-        const char* e = std::getenv("GOSSIP_PULL_GRID");
-        return e ? std::atoll(e) : 0ll;
-    }();
+uint64_t pull_grid_cap(bool nt, int64_t ov) {
     if (ov > 0) return (uint64_t)ov;
     return nt ? 16384ull : 2048ull;
-}
-
-// A/B knob: GOSSIP_PULL_LPW=16|32|64 forces the word-lanes per node of the sparse pull.
-int pull_lpw_override() {
-    static const int v = [] {
-        const char* e = std::getenv("GOSSIP_PULL_LPW");
-        const int x = e ? std::atoi(e) : 0;
-        return x == 16 || x == 32 || x == 64 ? x : 0;
-    }();
-    return v;
 }
 
 // Word-lanes per node of the sparse pull for windows wider than 64 words.  32 lanes (passes of
@@ -179,15 +154,10 @@ int pull_lpw_override() {
 // never ends in a half-idle 128-word pass) against 64 lanes, on the C4 / C3 benches
 // (profiles/r01/lanes_ab.json): C4 1216 words 127.7 -> 121.9 ms per launch, C4 8-shard 320 words
 // 44.0 -> 36.5 ms, C3 3.35 -> 3.06 ms; 16 lanes were slower on C4 (128.0 ms).
-int pull_lanes_per_node(uint32_t /*wact*/) {
-    if (const int ov = pull_lpw_override()) return ov;
-    return 32;
-}
+int pull_lanes_per_node(int64_t ov) { return ov == 16 || ov == 32 || ov == 64 ? (int)ov : 32; }
 
 template <int LPW, int EPN>
-void launch_pull_t(uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
-    const int ov = pull_nt_override();
-    const bool nt = ov >= 0 ? ov == 1 : (uint64_t)a.n * a.stride * 8u > kPullNtBytes;
+void launch_pull_t(bool nt, uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
     if constexpr ((LPW == 64 || LPW == 32 || LPW == 16) && EPN == 1) {
         if (nt) {
             k_pull<LPW, 1, true><<<grid, 256, lds, s>>>(a);
@@ -198,24 +168,34 @@ void launch_pull_t(uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) 
 }
 
 template <int LPW>
-void launch_pull_e(int epn, uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
+void launch_pull_e(int epn, bool nt, uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
     switch (epn) {
-        case 1: launch_pull_t<LPW, 1>(grid, lds, s, a); break;
-        case 2: launch_pull_t<LPW, 2>(grid, lds, s, a); break;
-        case 4: launch_pull_t<LPW, 4>(grid, lds, s, a); break;
-        case 8: launch_pull_t<LPW, 8>(grid, lds, s, a); break;
-        default: launch_pull_t<LPW, 8>(grid, lds, s, a); break;
+        case 1: launch_pull_t<LPW, 1>(nt, grid, lds, s, a); break;
+        case 2: launch_pull_t<LPW, 2>(nt, grid, lds, s, a); break;
+        case 4: launch_pull_t<LPW, 4>(nt, grid, lds, s, a); break;
+        case 8: launch_pull_t<LPW, 8>(nt, grid, lds, s, a); break;
+        default: launch_pull_t<LPW, 8>(nt, grid, lds, s, a); break;
     }
 }
 
 // (LPW, EPN) with 8 <= LPW, LPW * EPN <= 64, both powers of two.
-void launch_pull(int lpw, int epn, uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
+void launch_pull(int lpw, int epn, bool nt, uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
     switch (lpw) {  // lpw >= 8: one tile's 8 word-pairs sit in one lane group
-        case 8: launch_pull_e<8>(epn, grid, lds, s, a); break;
-        case 16: launch_pull_e<16>(epn, grid, lds, s, a); break;
-        case 32: launch_pull_e<32>(epn, grid, lds, s, a); break;
-        default: launch_pull_e<64>(epn, grid, lds, s, a); break;
+        case 8: launch_pull_e<8>(epn, nt, grid, lds, s, a); break;
+        case 16: launch_pull_e<16>(epn, nt, grid, lds, s, a); break;
+        case 32: launch_pull_e<32>(epn, nt, grid, lds, s, a); break;
+        default: launch_pull_e<64>(epn, nt, grid, lds, s, a); break;
     }
+}
+
+// GOSSIP_MODE_AUTO: the int8-MFMA contraction when the graph is dense enough that streaming its
+// bit adjacency (n^2/8 bytes per tick) beats gathering 128-B frontier rows per edge
+// (~16 B per (edge, word pair)): measured crossover in profiles/r02/auto_mode.jsonl -- p = 0.3
+// graphs at n = 4,096 - 65,536 run 5-19x faster on MFMA.  Needs the adjacency to fit in HBM
+// (n <= 2^19 here), and the handshake window's connector-only CSR has no MFMA form.
+bool auto_dense(uint32_t n, uint64_t nnz, bool handshake) {
+    if (handshake || n < 2048 || n > (1u << 19)) return false;
+    return (double)nnz >= 0.05 * (double)n * (double)n;
 }
 
 struct BirthArgs {
@@ -476,6 +456,12 @@ struct gossip_engine {
     hipEvent_t live_done[kRing] = {};
     bool live_pending[kRing] = {};
     int64_t live_tick[kRing] = {};
+    // ---- tuning options (gossip_engine_set_option; environment defaults)
+    int64_t opt_pull_nt = -1;         // -1 = by live footprint (kPullNtBytes), 0/1 forced
+    int64_t opt_pull_grid = 0;        // 0 = pull_grid_cap's default
+    int64_t opt_pull_lpw = 0;         // 0 = 32 word-lanes for wide windows
+    int64_t opt_dense_min_tiles = 512;  // block tiles the MFMA K split aims for
+    uint32_t last_nt = 0, last_grid = 0;  // variant of the last pull launch (counters)
     // ---- timing / counters
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers;
     std::vector<hipEvent_t> event_pool;
@@ -817,9 +803,22 @@ int gossip_engine::grow(uint32_t new_stride) {
     const uint64_t nb = (uint64_t)n * new_stride * 8;
     size_t freeb = 0, totalb = 0;
     HIP_TRY(hipMemGetInfo(&freeb, &totalb));
-    if (nb + (64ull << 20) > (uint64_t)freeb)
+    int ok = nb + (64ull << 20) <= (uint64_t)freeb ? 1 : 0;
+    if (comm) {
+        // Row-partitioned ranks widen in lockstep (their strides must agree for the exchange):
+        // all of them grow or all fail, never one rank alone while the others wait in the next
+        // exchange.
+        int* d_ok = reinterpret_cast<int*>(d_scalars);  // scratch word [0]
+        HIP_TRY(hipMemcpyAsync(d_ok, &ok, sizeof(int), hipMemcpyHostToDevice, stream));
+        if (ncclAllReduce(d_ok, d_ok, 1, ncclInt32, ncclMin, comm, stream) != ncclSuccess)
+            return set_error(GOSSIP_EHIP, "RCCL: capacity agreement failed");
+        HIP_TRY(hipMemcpyAsync(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+    }
+    if (!ok)
         return set_error(GOSSIP_ECAPACITY, "live-share window exceeded " + std::to_string(stride) +
-                                               " words per node and there is no device memory to widen it");
+                                               " words per node and there is no device memory to widen it" +
+                                               (comm ? " (on some rank of the row partition)" : ""));
     uint64_t** bufs[3] = {&d_F[0], &d_F[1], &d_seen};
     for (uint64_t** b : bufs) {
         uint64_t* nbuf = nullptr;
@@ -1130,11 +1129,14 @@ int gossip_engine::tick_step_a(int64_t t) {
         a.n = v1; a.stride = stride; a.wbase = 0; a.wact = wact;
         a.v0 = v0;  // row partition: this engine's rows [v0, v1)
         a.noskip = (cfg.flags & GOSSIP_F_NOSKIP) ? 1u : 0u;
-        const uint64_t chunks = ((uint64_t)n + 63) / 64;  // 64 nodes per wave step sequence
-        const int nt_ov = pull_nt_override();
-        const bool nt_rows = nt_ov >= 0 ? nt_ov == 1 : (uint64_t)v1 * stride * 8u > kPullNtBytes;
-        const uint32_t grid =
-            (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, pull_grid_cap(nt_rows)));
+        const uint64_t chunks = ((uint64_t)(v1 - v0) + 63) / 64;  // 64 nodes per wave step sequence
+        // non-temporal rows iff the frontier the launch gathers from (n rows x wact live words)
+        // exceeds kPullNtBytes
+        const bool nt_rows = opt_pull_nt >= 0 ? opt_pull_nt == 1 : (uint64_t)n * wact * 8u > kPullNtBytes;
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(
+            1, std::min<uint64_t>((chunks + 3) / 4, pull_grid_cap(nt_rows, opt_pull_grid)));
+        last_nt = nt_rows ? 1u : 0u;
+        last_grid = grid;
         const double avg_deg = n ? (double)nnz / n : 0.0;
         // One launch per kPullLdsWords words of the window (its per-word state lives in LDS).
         // Lane layout: word-lanes cover the launch's words in one pass when possible (at least
@@ -1149,7 +1151,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 while (lpw < 64 && 2 * lpw < (int)c.wact) lpw *= 2;
                 // windows wider than 64 words keep one peer walk per node (the pipelined path)
                 const bool wide_window = lpw == 64 && split_edges;
-                if (wide_window) lpw = pull_lanes_per_node(c.wact);
+                if (wide_window) lpw = pull_lanes_per_node(opt_pull_lpw);
                 int epn = 1;
                 while (split_edges && !wide_window && lpw * epn * 2 <= 64 && epn * 8 < avg_deg) epn *= 2;
                 // k_pull_wide (scalar peer loop) is opt-in: on C3 it measured 3.41 ms per launch
@@ -1159,7 +1161,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 if (wide)
                     k_pull_wide<<<grid, 256, pull_lds_bytes(c.wact), stream>>>(c);
                 else
-                    launch_pull(lpw, epn, grid, pull_lds_bytes(c.wact), stream, c);
+                    launch_pull(lpw, epn, nt_rows, grid, pull_lds_bytes(c.wact), stream, c);
             }
         };
         hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1186,7 +1188,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             gm.nt = wact / 4u;
             const uint32_t nst = n_pad / kStageK;
             uint32_t ks = 1;  // split K until the chip has ~2 tiles per CU (>= 2 stages per split)
-            const uint64_t min_tiles = dense_min_tiles();
+            const uint64_t min_tiles = (uint64_t)std::max<int64_t>(1, opt_dense_min_tiles);
             while ((uint64_t)gm.mb * gm.nt * ks < min_tiles && ks * 4 <= nst) ks *= 2;
             gm.ksplit = ks;
             gm.total = gm.mb * gm.nt * ks;
@@ -1382,6 +1384,10 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->tick_end = e->cut_r ? e->cut_tick + 1 : e->cut_tick;
         if (e->tick_end < e->tick0) e->tick_end = e->tick0;
         e->cur = e->tick0;
+        e->opt_pull_nt = env_option("GOSSIP_PULL_NT", -1);
+        e->opt_pull_grid = env_option("GOSSIP_PULL_GRID", 0);
+        e->opt_pull_lpw = env_option("GOSSIP_PULL_LPW", 0);
+        e->opt_dense_min_tiles = env_option("GOSSIP_DENSE_MIN_TILES", 512);
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
         e->dense = cfg->mode == GOSSIP_MODE_DENSE;
         e->handshake = (cfg->flags & GOSSIP_F_HANDSHAKE) != 0;
@@ -1444,6 +1450,7 @@ int gossip_engine_set_graph(gossip_engine* e, uint32_t num_nodes, const int64_t*
     HIP_TRY(hipMemcpy(e->d_rowptr, row_ptr, ((size_t)e->n + 1) * 8, hipMemcpyHostToDevice));
     if (e->nnz) HIP_TRY(hipMemcpy(e->d_col, col, e->nnz * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->d_deg, e->h_peers.data(), (size_t)e->n * 4, hipMemcpyHostToDevice));
+    if (e->cfg.mode == GOSSIP_MODE_AUTO) e->dense = auto_dense(e->n, e->nnz, e->handshake);
     if (e->dense) {
         // A[v][u] = [u in peers(v)] as bits (multiplicity only scales a count the pull does not
         // need), rows/cols padded to kDensePad with zeros.  Inc stays exact in int32 below 2^19
@@ -1622,6 +1629,28 @@ int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end
     return GOSSIP_OK;
 }
 
+int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) {
+    if (!e || !name) return set_error(GOSSIP_EINVAL, "NULL argument");
+    const std::string k(name);
+    if (k == "pull_nt") {
+        if (value < -1 || value > 1) return set_error(GOSSIP_EINVAL, "pull_nt: -1 (auto), 0 or 1");
+        e->opt_pull_nt = value;
+    } else if (k == "pull_grid") {
+        if (value < 0 || value > (1ll << 24)) return set_error(GOSSIP_EINVAL, "pull_grid: 0 (auto) .. 2^24 blocks");
+        e->opt_pull_grid = value;
+    } else if (k == "pull_lpw") {
+        if (value != 0 && value != 16 && value != 32 && value != 64)
+            return set_error(GOSSIP_EINVAL, "pull_lpw: 0 (auto), 16, 32 or 64");
+        e->opt_pull_lpw = value;
+    } else if (k == "dense_min_tiles") {
+        if (value < 1) return set_error(GOSSIP_EINVAL, "dense_min_tiles >= 1");
+        e->opt_dense_min_tiles = value;
+    } else {
+        return set_error(GOSSIP_EINVAL, "unknown option '" + k + "'");
+    }
+    return GOSSIP_OK;
+}
+
 int gossip_engine_set_link_timing(gossip_engine* e, int64_t ns_per_byte, uint32_t header_bytes,
                                   int64_t send_defer_ns) {
     if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
@@ -1752,6 +1781,11 @@ int gossip_engine_set_schedule_obj(gossip_engine* e, const gossip_schedule* s) {
 }
 
 int64_t gossip_engine_first_tick(const gossip_engine* e) { return e ? e->tick0 : -1; }
+int gossip_engine_mode(const gossip_engine* e) {
+    if (!e) return GOSSIP_EINVAL;
+    if (!e->have_graph && e->cfg.mode == GOSSIP_MODE_AUTO) return GOSSIP_MODE_AUTO;
+    return e->dense ? GOSSIP_MODE_DENSE : GOSSIP_MODE_CSR;
+}
 int64_t gossip_engine_end_tick(const gossip_engine* e) { return e ? e->tick_end : -1; }
 int64_t gossip_engine_current_tick(const gossip_engine* e) { return e ? e->cur : -1; }
 
@@ -1891,6 +1925,8 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     c->pull_seen_writes = acct[3];
     c->pull_f_writes = acct[4];
     c->pull_nz_reads = acct[7];
+    c->pull_nt = e->last_nt;
+    c->pull_grid = e->last_grid;
     uint64_t g = 0;
     const uint64_t done = (uint64_t)std::max<int64_t>(0, std::min(e->cur, e->tick_end) - e->tick0);
     if (!e->tick_lo.empty()) g = e->tick_lo[std::min<uint64_t>(done, e->tick_lo.size() - 1)];

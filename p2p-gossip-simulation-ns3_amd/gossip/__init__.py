@@ -55,6 +55,7 @@ EXPORTED_SYMBOLS = (
     "gossip_format_statistics", "gossip_format_periodic", "gossip_engine_set_link_timing",
     "gossip_share_message_length", "gossip_format_event_log", "gossip_engine_set_row_partition",
     "gossip_rccl_unique_id", "gossip_engine_connect_rccl", "gossip_engine_group_run",
+    "gossip_engine_set_option", "gossip_engine_mode",
 )
 
 # NS-3 5 Mbps point-to-point links (p2pnetwork.cc:113): ns per byte, PPP+IPv4+TCP(timestamp
@@ -65,7 +66,14 @@ GEN_EVENT_DTYPE = np.dtype([("ns", "<i8"), ("node", "<u4"), ("share_id", "<u4")]
 
 
 class GossipError(RuntimeError):
-    pass
+    """A failed C-ABI call; ``code`` is the GOSSIP_E* status (gossip.h)."""
+
+    def __init__(self, msg: str, code: int = 0):
+        super().__init__(msg)
+        self.code = code
+
+
+E_INVAL, E_HIP, E_NOMEM, E_STATE, E_CAPACITY = -1, -2, -3, -4, -5
 
 
 class gossip_config(C.Structure):
@@ -87,6 +95,7 @@ class gossip_counters(C.Structure):
         ("dense_tiles_skipped", C.c_uint64), ("pull_col_ids", C.c_uint64),
         ("pull_seen_reads", C.c_uint64), ("pull_seen_writes", C.c_uint64),
         ("pull_f_writes", C.c_uint64), ("pull_nz_reads", C.c_uint64),
+        ("pull_nt", C.c_uint32), ("pull_grid", C.c_uint32),
     ]
 
 
@@ -138,6 +147,8 @@ def load_library(path: str = LIB_PATH):
         "gossip_rccl_unique_id": (C.c_int, [C.c_char_p, u32]),
         "gossip_engine_connect_rccl": (C.c_int, [P, C.c_char_p, u32]),
         "gossip_engine_group_run": (C.c_int, [P, u32, i64]),
+        "gossip_engine_set_option": (C.c_int, [P, C.c_char_p, i64]),
+        "gossip_engine_mode": (C.c_int, [P]),
         "gossip_format_event_log": (i64, [P, u64, P, u64, P, P, P, P, i64, i64, i64, i64, u32,
                                           i64, C.c_int, C.c_char_p, u64]),
         "gossip_engine_first_tick": (i64, [P]),
@@ -165,7 +176,7 @@ def load_library(path: str = LIB_PATH):
 
 def _check(rc: int, what: str):
     if rc != 0:
-        raise GossipError(f"{what}: {load_library().gossip_last_error().decode()} (code {rc})")
+        raise GossipError(f"{what}: {load_library().gossip_last_error().decode()} (code {rc})", rc)
 
 
 def _vp(a):
@@ -334,6 +345,12 @@ class Engine:
         _check(load_library().gossip_engine_set_row_partition(self._h, int(rank), int(count)),
                "row partition")
 
+    def set_option(self, name: str, value: int):
+        """Tuning option (gossip.h gossip_engine_set_option): pull_nt, pull_grid, pull_lpw,
+        dense_min_tiles.  Results never depend on them."""
+        _check(load_library().gossip_engine_set_option(self._h, name.encode(), int(value)),
+               f"option {name}")
+
     def connect_rccl(self, unique_id: bytes):
         _check(load_library().gossip_engine_connect_rccl(self._h, unique_id, len(unique_id)),
                "rccl connect")
@@ -345,6 +362,11 @@ class Engine:
     def set_schedule(self, ev: np.ndarray):
         ev = np.ascontiguousarray(ev, GEN_EVENT_DTYPE)
         _check(load_library().gossip_engine_set_schedule(self._h, ev.size, _vp(ev)), "set schedule")
+
+    @property
+    def mode(self) -> int:
+        """MODE_CSR or MODE_DENSE (MODE_AUTO resolves when the graph is set)."""
+        return int(load_library().gossip_engine_mode(self._h))
 
     @property
     def first_tick(self) -> int:

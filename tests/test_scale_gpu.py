@@ -1,0 +1,289 @@
+"""The BASELINE.json configurations themselves under test on the GPU (C2, C4, C5), not just
+smaller stand-ins.
+
+C4 (10M nodes): a bounded sample replayed against ORACLE A bit for bit -- real generations of
+the bench's slice plus id groups built on the C4 graph (the id-collision paths of p2pnode.cc:189
+at full size) -- through every pull variant the bench can select (non-temporal rows, the 16,384-
+block grid, a grid of 3 blocks that makes every wave stride over thousands of chunks) and as two
+share shards; then the bench's own steady-state slice (shard 0 of 2, ~280 GiB) against the
+invariants of the reference's counters.
+C5 (65,536 nodes, p = 0.3, 4,096 concurrent shares): MFMA == CSR pull, a 64-share subset ==
+ORACLE B, row partitions of 2 and 8 ranks == the single engine.
+C2 (4,096 nodes, p = 0.3, full 60 s): MFMA tick-by-tick, MFMA hop-batched and the CSR pull ==
+ORACLE B over all ~64k shares.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+STATS = ("gen", "recv", "fwd", "sent", "processed", "peers", "sockets")
+SUM_STATS = ("gen", "recv", "fwd", "sent", "processed")
+
+
+def _w():
+    import gossip.workloads as W
+    return W
+
+
+def _same(st, ref, keys=STATS, what=""):
+    for k in keys:
+        a, b = getattr(st, k), getattr(ref, k)
+        assert np.array_equal(a, b), (what, k, int(np.count_nonzero(a != b)))
+
+
+def _run(gossip, topo, ev, t_start, t_cut, options=(), close=True, **kw):
+    eng = gossip.Engine(topo.num_nodes, _w().L_NS, t_start, t_cut, **kw)
+    for k, v in options:
+        eng.set_option(k, v)
+    eng.set_topology(topo)
+    eng.set_schedule(ev)
+    eng.run()
+    eng.sync()
+    st, c = eng.stats(), eng.counters()
+    if close:
+        eng.close()
+        return st, c
+    return st, c, eng
+
+
+def _sum(stats):
+    out = {}
+    for k in SUM_STATS:
+        out[k] = sum(getattr(s, k).astype(np.uint64) for s in stats)
+    return out
+
+
+def _invariants(st, c=None):
+    assert np.array_equal(st.fwd, st.recv)  # p2pnode.cc:157,163
+    assert np.array_equal(st.sent, st.peers.astype(np.uint64) * (st.gen + st.recv).astype(np.uint64))
+    assert np.all(st.processed <= st.gen + st.recv)
+    if c is not None:
+        assert c.edge_events == int(st.sent.sum())
+
+
+# ------------------------------------------------------------------------------------------- C4
+@pytest.fixture(scope="module")
+def c4(gossip):
+    W = _w()
+    topo = W.topology("C4")
+    rp, col, _ = topo.csr()
+    return topo, rp, col
+
+
+def _ring(rp, col, src, d):
+    """Nodes at exact BFS distance d from src (d small: the levels stay tiny)."""
+    seen = {int(src)}
+    level = [int(src)]
+    for _ in range(d):
+        nxt = []
+        for u in level:
+            for v in col[rp[u]:rp[u + 1]].tolist():
+                if v not in seen:
+                    seen.add(v)
+                    nxt.append(v)
+        level = nxt
+    return sorted(level)
+
+
+def _c4_sample(gossip, c4):
+    """Six real generations of the bench slice + five id groups placed on the C4 graph."""
+    W = _w()
+    topo, rp, col = c4
+    n = topo.num_nodes
+    L, T = W.L_NS, W.SLICE_NS
+    ev = gossip.make_schedule(n, W.CONFIGS["C4"]["node_seed"], W.T0_NS, W.T_CUT_NS,
+                              t_gen_end_ns=T + L, threads=16)
+    base = ev[ev["ns"] >= T][:6]
+    used = set(base["node"].tolist())
+    rows = []
+    gid = 0xC4C40000
+
+    def pick(cands):
+        for v in cands:
+            if v not in used:
+                used.add(v)
+                return v
+        raise AssertionError("no free node")
+
+    # deterministic anchors far apart in id space
+    anchors = [1_234_567, 3_456_789, 5_678_901, 7_890_123, 9_012_345]
+    t1 = T + L + 200_000  # tick 2001, phase 0.2 ms
+    # G1: the flood reaches b (distance 2) first, b generates 1 us later: gen + sent count,
+    #     processed does not (p2pnode.cc:115-120 with the id already in processedShares)
+    a = pick([anchors[0]]); b = pick(_ring(rp, col, a, 2))
+    rows += [(t1, a, gid), (t1 + 2 * L + 1000, b, gid)]
+    # G2: b generates 1 us BEFORE the flood's arrival in the same tick: the arrival is dropped
+    a = pick([anchors[1]]); b = pick(_ring(rp, col, a, 2))
+    rows += [(t1, a, gid + 1), (t1 + 2 * L - 1000, b, gid + 1)]
+    # G3: two floods of one id meet in the middle (distance 4, phases 500 ns apart)
+    a = pick([anchors[2]]); b = pick(_ring(rp, col, a, 4))
+    rows += [(t1, a, gid + 2), (t1 + 500, b, gid + 2)]
+    # G4: three sources in one tick, pairwise >= 2 hops apart, phases in reverse node order
+    a = pick([anchors[3]]); b = pick(_ring(rp, col, a, 2)); c = pick(_ring(rp, col, a, 3))
+    rows += [(t1 + 300_000, a, gid + 3), (t1 + 200_000, b, gid + 3), (t1 + 100_000, c, gid + 3)]
+    # G5: a tie -- b (a peer of a) generates at the very ns a's share arrives: the generation
+    #     event was scheduled first and wins
+    a = pick([anchors[4]]); b = pick(_ring(rp, col, a, 1))
+    rows += [(t1, a, gid + 4), (t1 + L, b, gid + 4)]
+    r = np.array(rows, dtype=np.int64)
+    grp = gossip.events_from_arrays(r[:, 0], r[:, 1], r[:, 2])
+    out = np.concatenate([base, grp])
+    out = out[np.lexsort((out["node"], out["ns"]))]
+    assert len(np.unique(base["share_id"])) == len(base) and not np.isin(grp["share_id"], base["share_id"]).any()
+    # PrintStatistics half-way through tick 2005: the base shares (tick 2000) count 5 hops, the
+    # groups (tick 2001) 4 hops if their phase is below L/2, else 3
+    return out, T + 5 * L + L // 2
+
+
+def test_c4_sample_matches_oracle_a(gossip, oracle, c4):
+    W = _w()
+    topo = c4[0]
+    n = topo.num_nodes
+    ev, t_cut = _c4_sample(gossip, c4)
+    a, b = topo.links()
+    ref = oracle.run_replay(n, W.L_NS, W.T0_NS, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
+    del a, b
+    assert ref.edge_events > 10_000_000 and int((ref.gen + ref.recv - ref.processed).sum()) >= 1
+    variants = [
+        ("auto", ()),
+        ("nt rows, 16384-block grid (the C4 production kernel)", (("pull_nt", 1), ("pull_grid", 16384))),
+        ("nt rows, 3-block grid", (("pull_nt", 1), ("pull_grid", 3))),
+        ("64 word-lanes", (("pull_lpw", 64),)),
+    ]
+    for name, opts in variants:
+        st, c = _run(gossip, topo, ev, W.T0_NS, t_cut, options=opts, max_words=16)
+        _same(st, ref, what=name)
+        if opts and opts[0] == ("pull_nt", 1):
+            assert c.pull_nt == 1 and c.pull_grid == dict(opts)["pull_grid"]
+    parts = [_run(gossip, topo, ev, W.T0_NS, t_cut, max_words=16, shard_rank=r, shard_count=2)[0]
+             for r in range(2)]
+    tot = _sum(parts)
+    for k in SUM_STATS:
+        assert np.array_equal(tot[k], getattr(ref, k).astype(np.uint64)), ("2 shards", k)
+
+
+def test_c4_bench_slice_invariants(gossip, c4):
+    # The bench's workload: shard 0 of 2 of the C4 slice (every generation of the 16 ticks before
+    # t = 10 s and of the timed ticks, plus all earlier generations of their ids), 5 warm-up +
+    # 20 timed ticks, ~280 GiB of device memory.
+    W = _w()
+    topo = c4[0]
+    n = topo.num_nodes
+    warm, steps = 5, 20
+    t_end = W.SLICE_NS + (warm + steps + 1) * W.L_NS
+    ev, info = W.slice_schedule(n, W.CONFIGS["C4"]["node_seed"], W.SLICE_NS, t_end)
+    assert info["earlier_same_id"] > 0
+    owner = gossip.shard_events(topo, ev, 2)
+    eng = gossip.Engine(n, W.L_NS, W.T0_NS, W.T_CUT_NS, shard_rank=0, shard_count=2)
+    eng.set_topology(topo)
+    eng.set_schedule(ev)
+    tick_end = W.SLICE_NS // W.L_NS + warm + steps
+    eng.run(tick_end)
+    eng.sync()
+    st, c = eng.stats(), eng.counters()
+    eng.close()
+    _invariants(st, c)
+    mine = ev[owner == 0]
+    gens = mine[mine["ns"] < tick_end * W.L_NS]
+    assert int(st.gen.sum()) == len(gens) == c.generations
+    assert np.array_equal(st.gen, np.bincount(gens["node"], minlength=n).astype(np.uint32))
+    # later generations of ids whose earlier flood already covered the node: counted, not processed
+    assert int((st.gen.astype(np.int64) + st.recv - st.processed).sum()) > 0
+    assert c.words_hw > 500 and int(st.recv.sum()) > 100 * len(gens)
+
+
+# ------------------------------------------------------------------------------------------- C5
+@pytest.fixture(scope="module")
+def c5(gossip):
+    W = _w()
+    return W.topology("C5"), W.c5_flood()
+
+
+def test_c5_mfma_equals_csr_and_oracle_b(gossip, oracle, c5):
+    W = _w()
+    topo, ev = c5
+    n = topo.num_nodes
+    t_cut = W.T0_NS + 40 * W.L_NS
+    dense, cd = _run(gossip, topo, ev, W.T0_NS, t_cut, mode=gossip.MODE_DENSE)
+    csr, _ = _run(gossip, topo, ev, W.T0_NS, t_cut, mode=gossip.MODE_CSR)
+    _same(dense, csr, what="C5 MFMA vs CSR, 4096 shares")
+    _invariants(dense, cd)
+    assert cd.dense_ops > 0 and int(dense.recv.sum()) == len(ev) * (n - 1)  # diameter 2: all reached
+    sub = ev[:64]
+    a, b = topo.links()
+    ref = oracle.run_oracle_b(n, W.L_NS, t_cut, a, b, sub["ns"], sub["node"], sub["share_id"], threads=16)
+    del a, b
+    for mode in (gossip.MODE_DENSE, gossip.MODE_CSR):
+        st, _ = _run(gossip, topo, sub, W.T0_NS, t_cut, mode=mode)
+        _same(st, ref, what=f"C5 64 shares mode {mode} vs ORACLE B")
+
+
+@pytest.mark.parametrize("ranks", [2, 8])
+def test_c5_row_partition_sums_to_single(gossip, c5, ranks):
+    W = _w()
+    topo, ev = c5
+    t_cut = W.T0_NS + 40 * W.L_NS
+    whole, _ = _run(gossip, topo, ev, W.T0_NS, t_cut, mode=gossip.MODE_DENSE)
+    engs = []
+    for r in range(ranks):
+        e = gossip.Engine(topo.num_nodes, W.L_NS, W.T0_NS, t_cut, mode=gossip.MODE_DENSE)
+        e.set_row_partition(r, ranks)
+        e.set_topology(topo)
+        e.set_schedule(ev)
+        engs.append(e)
+    gossip.group_run(engs)
+    parts = [e.stats() for e in engs]
+    for e in engs:
+        e.close()
+    tot = _sum(parts)
+    for k in SUM_STATS:
+        assert np.array_equal(tot[k], getattr(whole, k).astype(np.uint64)), (ranks, k)
+
+
+# ------------------------------------------------------------------------------------------- C2
+def test_c2_full_run_all_paths_match_oracle_b(gossip, oracle):
+    W = _w()
+    cfg = W.CONFIGS["C2"]
+    topo = W.topology("C2")
+    n = topo.num_nodes
+    ev = gossip.make_schedule(n, cfg["node_seed"], W.T0_NS, W.T_CUT_NS, threads=16)
+    a, b = topo.links()
+    ref = oracle.run_oracle_b(n, W.L_NS, W.T_CUT_NS, a, b, ev["ns"], ev["node"], ev["share_id"], threads=16)
+    assert ref.edge_events > 1e11
+    runs = [("MFMA tick-by-tick", dict(mode=gossip.MODE_DENSE)),
+            ("MFMA hop-batched", dict(mode=gossip.MODE_DENSE, flags=gossip.F_HOP_BATCH)),
+            ("CSR hop-batched", dict(mode=gossip.MODE_CSR, flags=gossip.F_HOP_BATCH)),
+            ("AUTO", dict())]
+    for name, kw in runs:
+        st, c = _run(gossip, topo, ev, W.T0_NS, W.T_CUT_NS, **kw)
+        _same(st, ref, what=name)
+        assert c.edge_events == ref.edge_events
+        if name == "AUTO":
+            assert c.dense_ops > 0  # AUTO picks the MFMA path on a p = 0.3 graph
+
+
+def test_c2_golden_fixture_on_every_path(gossip):
+    # tests/golden/n4096_p03_short (C2's graph shape, ORACLE A output): the MFMA contraction tick
+    # by tick and hop-batched, and the CSR pull, each bit-exact against the fixture
+    import golden_util as G
+    W = _w()
+    g = G.load("n4096_p03_short")
+    p = g["params"]
+    n = p["num_nodes"]
+    topo = gossip.Topology.gnp(n, p["connection_prob"], p["topo_seed"], gossip.TOPO_EXACT)
+    lat = gossip.milliseconds_to_ns(p["latency_ms"])
+    t_cut = gossip.seconds_to_ns(p["sim_time_s"] - 0.1)
+    ev = gossip.make_schedule(n, p["node_seed"], W.T0_NS, t_cut)
+    for kw in (dict(mode=gossip.MODE_DENSE), dict(mode=gossip.MODE_DENSE, flags=gossip.F_HOP_BATCH),
+               dict(mode=gossip.MODE_CSR), dict(mode=gossip.MODE_AUTO)):
+        eng = gossip.Engine(n, lat, W.T0_NS, t_cut, **kw)
+        eng.set_topology(topo)
+        eng.set_schedule(ev)
+        eng.run()
+        st = eng.stats()
+        if kw["mode"] == gossip.MODE_AUTO:
+            assert eng.mode == gossip.MODE_DENSE
+        eng.close()
+        for k in G.STAT_KEYS:
+            assert np.array_equal(getattr(st, k), g[k]), (kw, k)
