@@ -213,7 +213,13 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *                                                                         [GOSSIP_PULL_GRID]
  *   "pull_lpw"         word-lanes per node for windows > 64 words: 0 auto (32), 16, 32, 64
  *                                                                         [GOSSIP_PULL_LPW]
- *   "dense_min_tiles"  MFMA block tiles the K split aims for (512)  [GOSSIP_DENSE_MIN_TILES] */
+ *   "dense_min_tiles"  MFMA block tiles the K split aims for (512)  [GOSSIP_DENSE_MIN_TILES]
+ *   "young"            young-tile slots (k_pull_young): -1 auto (CSR tick engine, n >= 2^20),
+ *                      0 off, 1 on (before the schedule)                    [GOSSIP_YOUNG]
+ *   "young_age"        tiles stay in slots while their oldest shares are <= this many hops (4)
+ *                                                                          [GOSSIP_YOUNG_AGE]
+ *   "young_cap"        slot entries per node before it falls back to dense rows (1..127)
+ *                                                                          [GOSSIP_YOUNG_CAP] */
 int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value);
 /* The mode the engine runs (AUTO resolves at gossip_engine_set_graph). */
 int gossip_engine_mode(const gossip_engine* e);
@@ -260,6 +266,17 @@ typedef struct gossip_counters {
     uint64_t pull_nz_reads;    /* peer tile-occupancy words loaded [8 B]                */
     uint32_t pull_nt;          /* variant of the last pull launch: 1 = non-temporal rows */
     uint32_t pull_grid;        /* blocks of the last pull launch                        */
+    /* young tiles (k_pull_young) since reset; its time is NOT in pull_ms                  */
+    double young_ms;           /* summed HIP-event time of k_pull_young (TIMING)        */
+    uint64_t young_launches;
+    uint64_t young_bytes_moved;   /* bytes k_pull_young had to move                     */
+    uint64_t young_slot_lines;    /* peer slot lines read [128 B]                        */
+    uint64_t young_col_ids;       /* peer ids loaded [4 B]                               */
+    uint64_t young_fallback_rows; /* dense rows read from overflowed peers [128 B]       */
+    uint64_t young_seen_reads;    /* own seen words read [8 B]                           */
+    uint64_t young_seen_writes;   /* own seen words written [8 B]                        */
+    uint64_t young_rows_written;  /* dense tile rows written [128 B]                     */
+    uint64_t young_slot_writes;   /* slot lines written [128 B]                          */
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 int gossip_engine_reset_timing(gossip_engine* e);

@@ -71,6 +71,7 @@ struct Birth {
     uint32_t glen;   // group: number of bits
     uint32_t poff;   // group: offset of member phases in the per-tick phase buffer
     uint32_t flags;  // BF_*
+    uint32_t widx;   // write-sparse index of the birth's tile this tick (0xff: dense tile)
 };
 
 struct PullArgs {
@@ -127,6 +128,7 @@ __device__ __forceinline__ uint64_t group_fix(uint64_t nw, uint64_t seen, uint64
 
 #include "pull_kernel.h"
 #include "dense_kernel.h"
+#include "young_kernel.h"
 
 // Bitmaps above this size run k_pull<LPW,1> with non-temporal row accesses (pull_kernel.h).
 // The size is the launch's LIVE footprint, n x wact words (not the allocated capacity, which
@@ -216,7 +218,42 @@ struct BirthArgs {
     unsigned long long* nz;    // tile occupancy of Fnext (nullable: legacy zero-filled rows)
     uint32_t ntw;
     const uint32_t* degc;      // handshake window: connector-side |peers| (read only with BF_CONN)
+    uint16_t* slot;            // young tiles: F_next slots (young_kernel.h); null when off
+    uint32_t cap;              // slot capacity (entries)
+    const uint32_t* wt;        // write-sparse index -> tile, this tick
+    uint32_t nwt;
 };
+
+// Young-tile slot of a birth's node: the arrival bits of the group mask gm in word w (from the
+// slot entries; k_pull_young wrote them this tick), optionally tombstoning those entries.
+__device__ uint64_t slot_word_bits(uint16_t* s, uint32_t hdr, uint32_t widx, uint32_t wit, uint64_t gm,
+                                   bool remove) {
+    uint64_t r = 0ull;
+    for (uint32_t k = 1; k <= hdr; k++) {
+        const uint32_t e = s[k];
+        if (e == kSlotTomb || (e >> 10) != widx || ((e >> 6) & 15u) != wit) continue;
+        const uint64_t b = 1ull << (e & 63u);
+        if (!(b & gm)) continue;
+        r |= b;
+        if (remove) s[k] = (uint16_t)kSlotTomb;
+    }
+    return r;
+}
+
+// A slot that cannot take one more entry: expand it into dense rows of every write-sparse tile
+// (zeros included -- readers of an overflowed node read those rows without occupancy bits).
+__device__ void slot_spill(const BirthArgs& a, uint64_t v, uint16_t* s, uint32_t hdr) {
+    for (uint32_t q = 0; q < a.nwt; q++) {
+        uint64_t* row = a.Fnext + v * a.stride + (uint64_t)a.wt[q] * 16u;
+        for (uint32_t k = 0; k < 16; k++) row[k] = 0ull;
+    }
+    for (uint32_t k = 1; k <= hdr; k++) {
+        const uint32_t e = s[k];
+        if (e == kSlotTomb || (e >> 10) >= a.nwt) continue;
+        a.Fnext[v * a.stride + (uint64_t)a.wt[e >> 10] * 16u + ((e >> 6) & 15u)] |= 1ull << (e & 63u);
+    }
+    s[0] = (uint16_t)kSlotOverflow;
+}
 
 // GenerateAndGossipShare (p2pnode.cc:106-125): gen++, insert, send to all peers -- sends and
 // the generation count happen even when the id is already in processedShares.  At most one
@@ -238,6 +275,49 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
     const uint64_t bit = 1ull << (x.col & 63u);
     uint64_t* fp = a.Fnext + v * a.stride + w;
     uint64_t* sp = a.seen + v * a.stride + w;
+    if (x.widx != 0xffu && a.slot) {
+        // young tile (young_kernel.h): F_next of this node is its slot, unless overflowed
+        uint16_t* s = a.slot + v * kSlotU16;
+        uint32_t hdr = s[0];
+        const bool ovf = hdr == kSlotOverflow;
+        bool eff = true;
+        if (x.kind == BIRTH_GROUP) {
+            const uint64_t gm = (x.glen >= 64 ? ~0ull : ((1ull << x.glen) - 1ull)) << x.glo;
+            const uint64_t arr = ovf ? (*fp & gm) : slot_word_bits(s, hdr, x.widx, w & 15u, gm, false);
+            const uint64_t prior = (*sp & gm) & ~arr;
+            if (prior) {
+                eff = false;
+            } else if (arr) {
+                const int ab = __ffsll((long long)arr) - 1;
+                const int32_t aph = a.gphase[x.poff + (uint32_t)ab - x.glo];
+                if (aph < x.phase) {
+                    eff = false;
+                } else {
+                    if (ovf) *fp &= ~arr;
+                    else slot_word_bits(s, hdr, x.widx, w & 15u, arr, true);
+                    a.recv[v] -= 1u;
+                    a.sent[v] -= dv;
+                    if (a.snap && aph < a.snap_r) atomicAdd(a.snap, (unsigned long long)-1ll);
+                }
+            }
+        }
+        if (!eff) return;
+        if (!ovf && hdr >= a.cap) {
+            slot_spill(a, v, s, hdr);
+            hdr = kSlotOverflow;
+        }
+        if (hdr == kSlotOverflow) {
+            *fp |= bit;
+        } else {
+            s[1 + hdr] = (uint16_t)((x.widx << 10) | ((w & 15u) << 6) | (x.col & 63u));
+            s[0] = (uint16_t)(hdr + 1u);
+        }
+        *sp |= bit;
+        a.effgen[v] += 1u;
+        atomicOr(&a.live[w], (unsigned long long)bit);
+        if (a.snap && x.phase < a.snap_r) atomicAdd(a.snap, 1ull);
+        return;
+    }
     // Tile occupancy: a tile row the pull did not write this tick holds stale bits (it is
     // only ever read behind its occupancy bit), so the birth writes the whole row.
     const uint32_t tile = w >> 4;
@@ -338,6 +418,13 @@ struct Instance {
     uint32_t word = 0;
     uint8_t lo = 0;
     uint8_t state = 0;       // 0 unallocated, 1 live, 2 retired
+};
+
+// Per-tick young-tile control (young_kernel.h), uploaded through the staging ring.
+struct YoungPack {
+    YoungTile yt[kYoungMax];  // k_pull_young's tiles, sorted by tile
+    uint32_t wt[64];          // write-sparse index -> tile (births, spills)
+    uint8_t rmap[64];         // F_cur entry index -> position in yt (0xff: not read)
 };
 
 constexpr int kRing = 4;   // host staging slots
@@ -461,7 +548,21 @@ struct gossip_engine {
     int64_t opt_pull_grid = 0;        // 0 = pull_grid_cap's default
     int64_t opt_pull_lpw = 0;         // 0 = 32 word-lanes for wide windows
     int64_t opt_dense_min_tiles = 512;  // block tiles the MFMA K split aims for
+    int64_t opt_young = -1;           // young tiles (k_pull_young): -1 auto, 0 off, 1 on
+    int64_t opt_young_age = 4;        // write-sparse while the oldest shares are <= this many hops
+    int64_t opt_young_cap = 127;      // slot entries per node before it overflows to dense rows
     uint32_t last_nt = 0, last_grid = 0;  // variant of the last pull launch (counters)
+    // ---- young tiles (young_kernel.h)
+    bool young = false;
+    uint16_t* d_slot[2] = {nullptr, nullptr};  // per frontier buffer: n x kSlotU16
+    std::vector<int64_t> tile_first;           // tick of a tile's first birth
+    std::vector<uint8_t> tile_widx;            // write-sparse index of the last tick (0xff: none)
+    std::vector<uint32_t> wt_last;             // write-sparse index -> tile of the last tick
+    YoungPack* h_young[kRing] = {};
+    YoungPack* d_young[kRing] = {};
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timers_young;
+    double young_ms_done = 0.0;
+    uint64_t young_launches = 0;
     // ---- timing / counters
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers;
     std::vector<hipEvent_t> event_pool;
@@ -508,6 +609,12 @@ gossip_engine::~gossip_engine() {
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     hipFree(d_live_all);
+    hipFree(d_slot[0]); hipFree(d_slot[1]);
+    for (int k = 0; k < kRing; k++) { hipFree(d_young[k]); hipHostFree(h_young[k]); }
+    for (auto& p : timers_young) {
+        hipEventDestroy(p.first);
+        hipEventDestroy(p.second);
+    }
     if (comm) ncclCommDestroy(comm);
     for (int k = 0; k < kRing; k++) {
         hipFree(d_ctl[k]); hipFree(d_births[k]); hipFree(d_gphase[k]); hipFree(d_wflags[k]);
@@ -700,6 +807,15 @@ int gossip_engine::alloc_device() {
         words = (uint32_t)std::max<uint64_t>(w, 2);
     }
     stride = (words + kTileWords - 1) / kTileWords * kTileWords;  // rows start on 128-B lines
+    // Young tiles: the CSR tick pull on graphs whose frontier rows outgrow the caches (C3/C4).
+    {
+        const bool ok = !dense && !batch && !handshake && row_count == 1 && !(cfg.flags & GOSSIP_F_NOSKIP);
+        if (opt_young == 1 && !ok)
+            return set_error(GOSSIP_EINVAL, "young tiles need the CSR tick engine (not DENSE, HOP_BATCH, "
+                                            "HANDSHAKE, NOSKIP or a row partition)");
+        young = ok && (opt_young == 1 || (opt_young == -1 && n >= (1u << 20)));
+    }
+    const uint64_t slot_bytes = young ? 2ull * n * kSlotU16 * 2u : 0ull;
     size_t freeb = 0, totalb = 0;
     HIP_TRY(hipMemGetInfo(&freeb, &totalb));
     if (cfg.max_words == 0 && row_count == 1) {
@@ -710,7 +826,7 @@ int gossip_engine::alloc_device() {
         // card cannot be widened later (grow needs a fourth bitmap).  A C4 shard cut to a
         // 20-tick slice measured 1,200 words estimated and more needed.
         const uint64_t want = stride + std::max<uint64_t>(stride / 4, 2 * kTileWords);
-        const uint64_t other = (uint64_t)n * 24 + nnz * 4 + ((uint64_t)n + 1) * 8 +
+        const uint64_t other = (uint64_t)n * 24 + nnz * 4 + ((uint64_t)n + 1) * 8 + slot_bytes +
                                16ull * n * ((want + 1023u) / 1024u) + (4ull << 30);  // + RCCL / context
         const uint64_t per_word = 3ull * n * 8 + (dense ? 8ull * n_pad : 0ull);
         uint64_t fit = freeb > other ? ((uint64_t)freeb - other) / per_word : 0ull;
@@ -718,7 +834,7 @@ int gossip_engine::alloc_device() {
         stride = (uint32_t)std::max<uint64_t>(stride, std::min<uint64_t>(want / kTileWords * kTileWords, fit));
     }
     const uint64_t bm = (uint64_t)n * stride * 8;
-    const uint64_t need = 3 * bm + (uint64_t)n * 24 + (nnz * 4) + ((uint64_t)n + 1) * 8 +
+    const uint64_t need = 3 * bm + (uint64_t)n * 24 + (nnz * 4) + ((uint64_t)n + 1) * 8 + slot_bytes +
                           (dense ? (uint64_t)stride * 8 * n_pad : 0ull);
     if (need > (uint64_t)freeb)
         return set_error(GOSSIP_ENOMEM, "device memory: need " + std::to_string(need) +
@@ -753,8 +869,18 @@ int gossip_engine::alloc_device() {
     const size_t nsc = 2 + 2 * snaps.size();
     HIP_TRY(hipMalloc(&d_scalars, nsc * 8));
     HIP_TRY(hipMemsetAsync(d_scalars, 0, nsc * 8, stream));
-    HIP_TRY(hipMalloc(&d_acct, 8 * 8));
-    HIP_TRY(hipMemsetAsync(d_acct, 0, 8 * 8, stream));
+    HIP_TRY(hipMalloc(&d_acct, 16 * 8));
+    HIP_TRY(hipMemsetAsync(d_acct, 0, 16 * 8, stream));
+    if (young) {
+        for (int k = 0; k < 2; k++) {
+            HIP_TRY(hipMalloc(&d_slot[k], (size_t)n * kSlotU16 * 2u));
+            HIP_TRY(hipMemsetAsync(d_slot[k], 0, (size_t)n * kSlotU16 * 2u, stream));
+        }
+        for (int k = 0; k < kRing; k++) {
+            HIP_TRY(hipMalloc(&d_young[k], sizeof(YoungPack)));
+            HIP_TRY(hipHostMalloc(&h_young[k], sizeof(YoungPack), hipHostMallocDefault));
+        }
+    }
     const uint32_t bcap = std::max<uint32_t>(max_births, 1);
     const uint32_t pcap = std::max<uint32_t>(max_group_phases, 1);
     for (int k = 0; k < kRing; k++) {
@@ -770,7 +896,7 @@ int gossip_engine::alloc_device() {
         HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&live_done[k], hipEventDisableTiming));
     }
-    device_bytes = 3 * bm + 16ull * n * ntw + (uint64_t)n * 20 + nnz * 4 + ((uint64_t)n + 1) * 8 + 2ull * stride * 8 +
+    device_bytes = 3 * bm + 16ull * n * ntw + (uint64_t)n * 20 + nnz * 4 + ((uint64_t)n + 1) * 8 + 2ull * stride * 8 + slot_bytes +
                    kRing * ((uint64_t)stride * sizeof(WordCtl) + (uint64_t)bcap * sizeof(Birth) + pcap * 4);
     if (dense) {
         const uint64_t ft = (uint64_t)stride * 8 * n_pad;
@@ -789,6 +915,8 @@ int gossip_engine::alloc_device() {
     ctl.assign(stride, z);
     tile_alloc.assign(stride / kTileWords, 0);
     tile_last_inject.assign(stride / kTileWords, INT64_MIN);
+    tile_first.assign(stride / kTileWords, INT64_MIN);
+    tile_widx.assign(stride / kTileWords, 0xffu);
     word_insts.assign(stride, {});
     col_phase.assign((size_t)stride * 64, 0);
     col_src.assign((size_t)stride * 64, UINT32_MAX);
@@ -897,6 +1025,8 @@ int gossip_engine::grow(uint32_t new_stride) {
     ctl.resize(new_stride, z);
     tile_alloc.resize(new_stride / kTileWords, 0);
     tile_last_inject.resize(new_stride / kTileWords, INT64_MIN);
+    tile_first.resize(new_stride / kTileWords, INT64_MIN);
+    tile_widx.resize(new_stride / kTileWords, 0xffu);
     word_insts.resize(new_stride);
     col_phase.resize((size_t)new_stride * 64, 0);
     col_src.resize((size_t)new_stride * 64, UINT32_MAX);
@@ -932,6 +1062,7 @@ int gossip_engine::alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t
             hw += kTileWords;
         }
         tile_alloc[tl] = 1;
+        tile_first[tl] = t;
         for (uint32_t q = 0; q < kTileWords; q++) reset_now.push_back(tl * kTileWords + q);
         open_tile = tl;
         open_word_in_tile = 0;
@@ -1050,6 +1181,59 @@ int gossip_engine::tick_step_a(int64_t t) {
         }
         if (e.node >= v0 && e.node < v1) B[nb++] = b;  // row partition: own nodes only
     }
+    // 3b. young tiles of this tick (young_kernel.h): every tile F_cur holds in slots (it was
+    //     write-sparse last tick) plus fresh tiles opened by this tick's births; the youngest of
+    //     them stay (or become) write-sparse while their oldest shares are <= young_age hops old.
+    uint32_t ny = 0, nwt = 0;
+    YoungPack* YP = young ? h_young[slot] : nullptr;
+    std::vector<uint8_t> new_widx;
+    if (young) {
+        const uint32_t ntiles = hw / kTileWords;
+        struct Cand {
+            uint32_t tile;
+            bool rd;
+            int64_t first;
+        };
+        std::vector<Cand> cand;
+        uint32_t nrd = 0;
+        for (uint32_t tl = 0; tl < ntiles; tl++) {
+            if (!tile_alloc[tl]) continue;
+            const bool rd = tile_widx[tl] != 0xffu;
+            const bool fresh = tile_first[tl] == t && t + 1 - tile_first[tl] <= opt_young_age;
+            if (rd || fresh) cand.push_back(Cand{tl, rd, tile_first[tl]});
+            nrd += rd;
+        }
+        std::sort(cand.begin(), cand.end(), [](const Cand& a, const Cand& b) {
+            return a.first != b.first ? a.first > b.first : a.tile < b.tile;  // youngest first
+        });
+        new_widx.assign(tile_widx.size(), 0xffu);
+        std::fill(YP->rmap, YP->rmap + 64, (uint8_t)0xffu);
+        uint32_t fresh_room = kYoungMax > nrd ? kYoungMax - nrd : 0u;  // nrd <= kYoungWriteMax < kYoungMax
+        for (const Cand& c : cand) {
+            const bool wr_age = t + 1 - c.first <= opt_young_age && nwt < kYoungWriteMax;
+            if (!c.rd) {
+                if (!wr_age || fresh_room == 0) continue;  // stays a dense tile (it is dead this tick)
+                fresh_room--;
+            }
+            YoungTile y{c.tile, (uint8_t)((c.rd ? YT_READ : 0u) | (wr_age ? YT_WRITE : 0u)),
+                        c.rd ? tile_widx[c.tile] : (uint8_t)0xffu, (uint8_t)0xffu, 0};
+            if (wr_age) {
+                y.w_idx = (uint8_t)nwt;
+                YP->wt[nwt++] = c.tile;
+                new_widx[c.tile] = y.w_idx;
+            }
+            YP->yt[ny++] = y;
+        }
+        std::sort(YP->yt, YP->yt + ny, [](const YoungTile& a, const YoungTile& b) { return a.tile < b.tile; });
+        for (uint32_t i = 0; i < ny; i++)
+            if (YP->yt[i].flags & YT_READ) YP->rmap[YP->yt[i].r_idx] = (uint8_t)i;
+        for (uint32_t q = 0; q < nb; q++) {
+            const uint32_t tl = B[q].col >> 10;
+            B[q].widx = tl < new_widx.size() ? new_widx[tl] : 0xffu;
+        }
+    } else {
+        for (uint32_t q = 0; q < nb; q++) B[q].widx = 0xffu;
+    }
     // 4. per-word control for this tick
     for (uint32_t w : reset_now) ctl[w].clear = ~0ull;
     const bool is_cut = (t == cut_tick && cut_r > 0);
@@ -1098,6 +1282,8 @@ int gossip_engine::tick_step_a(int64_t t) {
         WF[w] = (uint8_t)((c.clear ? WF_CLEAR : 0u) | (c.gmask ? WF_GROUP : 0u) |
                           (c.keep != ~0ull ? WF_KEEP : 0u) | (c.snap ? WF_SNAP : 0u));
     }
+    for (uint32_t i = 0; i < ny; i++)  // k_pull leaves these words to k_pull_young
+        for (uint32_t q = 0; q < kTileWords; q++) WF[YP->yt[i].tile * kTileWords + q] |= (uint8_t)WF_YOUNG;
     for (uint32_t w : reset_now) ctl[w].clear = 0ull;
     // 5. upload + launches
     const uint32_t wact = hw;
@@ -1106,6 +1292,7 @@ int gossip_engine::tick_step_a(int64_t t) {
     if (nb) HIP_TRY(hipMemcpyAsync(d_births[slot], B, (size_t)nb * sizeof(Birth), hipMemcpyHostToDevice, stream));
     if (np) HIP_TRY(hipMemcpyAsync(d_gphase[slot], GP, (size_t)np * 4, hipMemcpyHostToDevice, stream));
     if (smask_any) HIP_TRY(hipMemcpyAsync(d_smask[slot], h_smask[slot], nsnap * hw * 8, hipMemcpyHostToDevice, stream));
+    if (ny) HIP_TRY(hipMemcpyAsync(d_young[slot], YP, sizeof(YoungPack), hipMemcpyHostToDevice, stream));
     HIP_TRY(hipEventRecord(slot_done[slot], stream));
     const int lv = (int)(t % 3);
     if (wact) HIP_TRY(hipMemsetAsync(d_live[lv], 0, (size_t)wact * 8, stream));
@@ -1206,6 +1393,33 @@ int gossip_engine::tick_step_a(int64_t t) {
                 HIP_TRY(hipEventRecord(e1, stream));
                 timers.emplace_back(e0, e1);
             }
+            if (ny) {  // the young tiles (young_kernel.h), after k_pull wrote the nz words
+                YoungArgs y;
+                y.rowptr = a.rowptr; y.col = a.col; y.deg = d_deg;
+                y.Fcur = d_F[fcur]; y.Fnext = d_F[nxt]; y.seen = d_seen;
+                y.slot_cur = d_slot[fcur]; y.slot_next = d_slot[nxt];
+                y.ctl = d_ctl[slot]; y.wflags = d_wflags[slot];
+                y.recv = d_recv; y.sent = d_sent; y.live = d_live[lv]; y.live_prev = a.live_prev;
+                y.snap = snap_ptr; y.acct = d_acct; y.nz_next = d_nz[nxt]; y.ntw = ntw;
+                y.yt = d_young[slot]->yt; y.ny = ny; y.rmap = d_young[slot]->rmap;
+                y.n = v1; y.v0 = v0; y.stride = stride;
+                y.cap = (uint32_t)std::min<int64_t>(kSlotU16 - 1, std::max<int64_t>(1, opt_young_cap));
+                const uint32_t yg = (uint32_t)std::max<uint64_t>(
+                    1, std::min<uint64_t>(((uint64_t)(v1 - v0) + 3) / 4, pull_grid_cap(nt_rows, opt_pull_grid)));
+                hipEvent_t y0 = nullptr, y1 = nullptr;
+                if (cfg.flags & GOSSIP_F_TIMING) {
+                    y0 = get_event();
+                    y1 = get_event();
+                    HIP_TRY(hipEventRecord(y0, stream));
+                }
+                k_pull_young<<<yg, 256, young_lds_bytes(ny), stream>>>(y);
+                HIP_TRY(hipGetLastError());
+                if (cfg.flags & GOSSIP_F_TIMING) {
+                    HIP_TRY(hipEventRecord(y1, stream));
+                    timers_young.emplace_back(y0, y1);
+                }
+                young_launches++;
+            }
         }
         HIP_TRY(hipGetLastError());
         pull_launches++;
@@ -1220,8 +1434,16 @@ int gossip_engine::tick_step_a(int64_t t) {
         b.nz = d_nz[nxt];
         b.ntw = ntw;
         b.degc = d_degc;
+        b.slot = (young && nwt) ? d_slot[nxt] : nullptr;
+        b.cap = (uint32_t)std::min<int64_t>(kSlotU16 - 1, std::max<int64_t>(1, opt_young_cap));
+        b.wt = young ? d_young[slot]->wt : nullptr;
+        b.nwt = nwt;
         k_births<<<(nb + 255) / 256, 256, 0, stream>>>(b);
         HIP_TRY(hipGetLastError());
+    }
+    if (young) {  // F_next's slots hold this tick's write-sparse tiles: next tick reads them
+        tile_widx.swap(new_widx);
+        wt_last.assign(YP->wt, YP->wt + nwt);
     }
     if (smask_any) {  // hop-batched snapshots: arrivals of this tick that precede each snapshot
         const uint64_t cells = (uint64_t)(v1 - v0) * hw;
@@ -1331,10 +1553,28 @@ int gossip_engine::decode_trace(int64_t t) {
         nz.resize((size_t)n * ntw);
         HIP_TRY(hipMemcpy(nz.data(), d_nz[fcur], nz.size() * 8, hipMemcpyDeviceToHost));
     }
+    // young tiles: F_{t+1} of the write-sparse tiles lives in the slots (unless overflowed)
+    std::vector<uint8_t> ws_tile(stride / kTileWords, 0);
+    if (young && !wt_last.empty()) {
+        for (uint32_t tl : wt_last) ws_tile[tl] = 1;
+        std::vector<uint16_t> S((size_t)n * kSlotU16);
+        HIP_TRY(hipMemcpy(S.data(), d_slot[fcur], S.size() * 2, hipMemcpyDeviceToHost));
+        for (uint32_t v = v0; v < v1; v++) {
+            const uint16_t* sv = S.data() + (size_t)v * kSlotU16;
+            if (sv[0] == kSlotOverflow) continue;  // dense rows valid
+            for (uint32_t tl : wt_last)
+                for (uint32_t q = 0; q < kTileWords; q++) F[(size_t)v * stride + tl * kTileWords + q] = 0ull;
+            for (uint32_t k = 1; k <= sv[0]; k++) {
+                const uint32_t e = sv[k];
+                if (e == kSlotTomb || (e >> 10) >= wt_last.size()) continue;
+                F[(size_t)v * stride + wt_last[e >> 10] * kTileWords + ((e >> 6) & 15u)] |= 1ull << (e & 63u);
+            }
+        }
+    }
     for (uint32_t v = v0; v < v1; v++)
         for (uint32_t w = 0; w < hw; w++) {
             const uint32_t tl = w >> 4;
-            if (!nz.empty() && !((nz[(size_t)v * ntw + (tl >> 6)] >> (tl & 63u)) & 1ull)) continue;  // stale row
+            if (!nz.empty() && !ws_tile[tl] && !((nz[(size_t)v * ntw + (tl >> 6)] >> (tl & 63u)) & 1ull)) continue;  // stale row
             uint64_t x = F[(size_t)v * stride + w];
             while (x) {
                 const int b = __builtin_ctzll(x);
@@ -1388,6 +1628,9 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_pull_grid = env_option("GOSSIP_PULL_GRID", 0);
         e->opt_pull_lpw = env_option("GOSSIP_PULL_LPW", 0);
         e->opt_dense_min_tiles = env_option("GOSSIP_DENSE_MIN_TILES", 512);
+        e->opt_young = env_option("GOSSIP_YOUNG", -1);
+        e->opt_young_age = env_option("GOSSIP_YOUNG_AGE", 4);
+        e->opt_young_cap = env_option("GOSSIP_YOUNG_CAP", 127);
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
         e->dense = cfg->mode == GOSSIP_MODE_DENSE;
         e->handshake = (cfg->flags & GOSSIP_F_HANDSHAKE) != 0;
@@ -1642,6 +1885,16 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
         if (value != 0 && value != 16 && value != 32 && value != 64)
             return set_error(GOSSIP_EINVAL, "pull_lpw: 0 (auto), 16, 32 or 64");
         e->opt_pull_lpw = value;
+    } else if (k == "young") {
+        if (value < -1 || value > 1) return set_error(GOSSIP_EINVAL, "young: -1 (auto), 0 or 1");
+        if (e->have_sched) return set_error(GOSSIP_ESTATE, "young: set before the schedule");
+        e->opt_young = value;
+    } else if (k == "young_age") {
+        if (value < 1 || value > 64) return set_error(GOSSIP_EINVAL, "young_age: 1 .. 64 hops");
+        e->opt_young_age = value;
+    } else if (k == "young_cap") {
+        if (value < 1 || value > (int64_t)kSlotU16 - 1) return set_error(GOSSIP_EINVAL, "young_cap: 1 .. 127 entries");
+        e->opt_young_cap = value;
     } else if (k == "dense_min_tiles") {
         if (value < 1) return set_error(GOSSIP_EINVAL, "dense_min_tiles >= 1");
         e->opt_dense_min_tiles = value;
@@ -1907,7 +2160,7 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     HIP_TRY(hipGetLastError());
     unsigned long long v[2];
     HIP_TRY(hipMemcpyAsync(v, e->d_scalars, 16, hipMemcpyDeviceToHost, e->stream));
-    unsigned long long acct[8] = {0};
+    unsigned long long acct[16] = {0};
     HIP_TRY(hipMemcpyAsync(acct, e->d_acct, sizeof(acct), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     c->edge_events = v[0];
@@ -1927,6 +2180,31 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     c->pull_nz_reads = acct[7];
     c->pull_nt = e->last_nt;
     c->pull_grid = e->last_grid;
+    {
+        double yms = e->young_ms_done;
+        for (auto& p : e->timers_young) {
+            float x = 0.f;
+            HIP_TRY(hipEventElapsedTime(&x, p.first, p.second));
+            yms += x;
+            e->event_pool.push_back(p.first);
+            e->event_pool.push_back(p.second);
+        }
+        e->timers_young.clear();
+        e->young_ms_done = yms;
+        c->young_ms = yms;
+    }
+    c->young_launches = e->young_launches;
+    c->young_slot_lines = acct[8];
+    c->young_col_ids = acct[9];
+    c->young_fallback_rows = acct[10];
+    c->young_seen_reads = acct[11];
+    c->young_seen_writes = acct[12];
+    c->young_rows_written = acct[13];
+    c->young_slot_writes = acct[14];
+    // k_pull_young's bytes: 128 B per slot line / fallback row / row written / slot written,
+    // 4 B per peer id, 8 B per own seen word, row_ptr + counters per node and launch
+    c->young_bytes_moved = 128ull * (acct[8] + acct[10] + acct[13] + acct[14]) + 4ull * acct[9] +
+                           8ull * (acct[11] + acct[12]) + e->young_launches * (8ull * (e->n + 1) + 16ull * e->n);
     uint64_t g = 0;
     const uint64_t done = (uint64_t)std::max<int64_t>(0, std::min(e->cur, e->tick_end) - e->tick0);
     if (!e->tick_lo.empty()) g = e->tick_lo[std::min<uint64_t>(done, e->tick_lo.size() - 1)];
@@ -1946,8 +2224,15 @@ int gossip_engine_reset_timing(gossip_engine* e) {
     e->pull_ms_done = 0.0;
     e->pull_launches = 0;
     e->pull_bytes = 0;
+    for (auto& p : e->timers_young) {
+        e->event_pool.push_back(p.first);
+        e->event_pool.push_back(p.second);
+    }
+    e->timers_young.clear();
+    e->young_ms_done = 0.0;
+    e->young_launches = 0;
     if (e->d_acct) {
-        HIP_TRY(hipMemsetAsync(e->d_acct, 0, 8 * 8, e->stream));
+        HIP_TRY(hipMemsetAsync(e->d_acct, 0, 16 * 8, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));
     }
     return GOSSIP_OK;

@@ -45,7 +45,8 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 // Lanes of the wave for which c holds (a wave-uniform value: traffic accounting in SGPRs).
 __device__ __forceinline__ uint32_t wave_count(bool c) { return (uint32_t)__popcll(__ballot(c)); }
 
-enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u };
+// WF_YOUNG: the word belongs to a young tile, which k_pull_young owns this tick (young_kernel.h)
+enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u, WF_YOUNG = 16u };
 
 constexpr uint32_t kPullLdsWords = 2048;  // words per launch: LDS liveness, new liveness, flags
 #ifndef PULL_INFLIGHT
@@ -118,9 +119,11 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     unsigned long long* s_new = smem + a.wact;   // liveness of this tick (OR of new bits)
     uint8_t* s_wf = reinterpret_cast<uint8_t*>(smem + 2u * a.wact);
     for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
-        s_lp[i] = (a.live_prev && !a.noskip) ? a.live_prev[a.wbase + i] : ~0ull;
+        const uint8_t f = a.wflags[a.wbase + i];
+        // a young word is k_pull_young's: dead here, no clear, no write
+        s_lp[i] = (f & WF_YOUNG) ? 0ull : (a.live_prev && !a.noskip) ? a.live_prev[a.wbase + i] : ~0ull;
         s_new[i] = 0ull;
-        s_wf[i] = a.wflags[a.wbase + i];
+        s_wf[i] = (f & WF_YOUNG) ? (uint8_t)0 : f;
     }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -448,9 +451,11 @@ __global__ __launch_bounds__(256) void k_pull_wide(PullArgs a) {
     unsigned long long* s_new = smem + a.wact;
     uint8_t* s_wf = reinterpret_cast<uint8_t*>(smem + 2u * a.wact);
     for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
-        s_lp[i] = (a.live_prev && !a.noskip) ? a.live_prev[a.wbase + i] : ~0ull;
+        const uint8_t f = a.wflags[a.wbase + i];
+        // a young word is k_pull_young's: dead here, no clear, no write
+        s_lp[i] = (f & WF_YOUNG) ? 0ull : (a.live_prev && !a.noskip) ? a.live_prev[a.wbase + i] : ~0ull;
         s_new[i] = 0ull;
-        s_wf[i] = a.wflags[a.wbase + i];
+        s_wf[i] = (f & WF_YOUNG) ? (uint8_t)0 : f;
     }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;

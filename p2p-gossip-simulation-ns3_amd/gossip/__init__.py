@@ -96,6 +96,11 @@ class gossip_counters(C.Structure):
         ("pull_seen_reads", C.c_uint64), ("pull_seen_writes", C.c_uint64),
         ("pull_f_writes", C.c_uint64), ("pull_nz_reads", C.c_uint64),
         ("pull_nt", C.c_uint32), ("pull_grid", C.c_uint32),
+        ("young_ms", C.c_double), ("young_launches", C.c_uint64),
+        ("young_bytes_moved", C.c_uint64), ("young_slot_lines", C.c_uint64),
+        ("young_col_ids", C.c_uint64), ("young_fallback_rows", C.c_uint64),
+        ("young_seen_reads", C.c_uint64), ("young_seen_writes", C.c_uint64),
+        ("young_rows_written", C.c_uint64), ("young_slot_writes", C.c_uint64),
     ]
 
 

@@ -1,0 +1,121 @@
+"""Young-tile slots (k_pull_young, young_kernel.h) against ORACLE A.
+
+Young tiles are switched on by default only for n >= 2^20 (C3/C4); here they are forced on small
+graphs, with a fresh tile every tick (so every tick has young, leaving and fresh tiles), tiny slot
+capacities (so nodes overflow to dense rows, in the pull and in the births), every young age, and
+forced id collisions (id-group births that must find or cancel arrivals inside slots).  Per-node
+counters and the first-contact trace must equal the oracle's bit for bit.
+"""
+import numpy as np
+import pytest
+
+from cases import T0
+
+pytestmark = pytest.mark.gpu
+
+STATS = ("gen", "recv", "fwd", "sent", "processed", "peers", "sockets")
+
+
+def _run(gossip, topo, ev, lat, t_cut, opts, flags=0, snapshots=()):
+    eng = gossip.Engine(topo.num_nodes, lat, T0, t_cut, flags=flags)
+    for k, v in opts.items():
+        eng.set_option(k, v)
+    eng.set_topology(topo)
+    for s in snapshots:
+        eng.add_snapshot(s)
+    eng.set_schedule(ev)
+    eng.run()
+    eng.sync()
+    return eng
+
+
+def _parity(gossip, oracle, n, p, seed, sim_s, lat_ms, opts, id_mask=0, flags=0, trace=True):
+    topo = gossip.Topology.gnp(n, p, seed, gossip.TOPO_SKIP if n > 5000 else gossip.TOPO_EXACT)
+    lat = gossip.milliseconds_to_ns(lat_ms)
+    t_cut = gossip.seconds_to_ns(sim_s - 0.1)
+    ev = gossip.make_schedule(n, seed + 1, T0, t_cut, id_mask=id_mask)
+    f = flags | (gossip.F_TRACE if trace else 0)
+    eng = _run(gossip, topo, ev, lat, t_cut, dict(opts, young=1), flags=f)
+    st = eng.stats()
+    c = eng.counters()
+    a, b = topo.links()
+    r = oracle.run_replay(n, lat, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=trace)
+    for k in STATS:
+        assert np.array_equal(getattr(st, k), getattr(r, k)), (opts, k)
+    if trace:
+        node, sid, tick, hop, via = eng.trace()
+        tn, ti, tt, th, tv = r.trace
+        ek, ok = np.lexsort((sid, node)), np.lexsort((ti, tn))
+        assert np.array_equal(node[ek], tn[ok]) and np.array_equal(sid[ek], ti[ok])
+        assert np.array_equal(tick[ek], tt[ok] // lat) and np.array_equal(hop[ek], th[ok])
+        assert np.array_equal(via[ek], tv[ok])
+    eng.close()
+    return c
+
+
+@pytest.mark.parametrize("cap", [1, 3, 127])
+@pytest.mark.parametrize("age", [1, 3, 6])
+def test_young_sparse_4096(gossip, oracle, cap, age):
+    c = _parity(gossip, oracle, 4096, 16.0 / 4095, 71, 6.0, 5.0,
+                dict(young_cap=cap, young_age=age), flags=gossip.F_TILE_PER_TICK)
+    assert c.young_launches > 0 and c.young_slot_lines > 0
+    if cap == 1:
+        assert c.young_fallback_rows > 0  # overflowed peers were read through dense rows
+
+
+@pytest.mark.parametrize("cap", [2, 127])
+def test_young_collisions(gossip, oracle, cap):
+    # 0x3FF id mask: id groups of several sources; group births resolve against slot arrivals
+    _parity(gossip, oracle, 400, 0.01, 73, 15.0, 5.0, dict(young_cap=cap, young_age=4),
+            id_mask=0x3FF, flags=gossip.F_TILE_PER_TICK)
+
+
+def test_young_collisions_shared_tiles(gossip, oracle):
+    # without a tile per tick: several ticks of births share one open tile
+    _parity(gossip, oracle, 600, 0.008, 74, 12.0, 5.0, dict(young_cap=4, young_age=5), id_mask=0x7FF)
+
+
+def test_young_odd_latency_cut(gossip, oracle):
+    # a cut inside a tick (keep masks on young words) and a latency that does not divide 1 s
+    _parity(gossip, oracle, 3000, 10.0 / 2999, 75, 7.37, 2.3, dict(young_cap=16, young_age=3),
+            flags=gossip.F_TILE_PER_TICK)
+
+
+def test_young_dense_graph(gossip, oracle):
+    # p = 0.3: hundreds of peers per node (the gather walks several 64-peer chunks)
+    _parity(gossip, oracle, 700, 0.3, 76, 5.6, 5.0, dict(young_cap=64, young_age=2),
+            flags=gossip.F_TILE_PER_TICK)
+
+
+def test_young_periodic_snapshots(gossip, oracle, monkeypatch):
+    # PrintPeriodicStats partials counted inside k_pull_young (WF_SNAP) and k_births
+    monkeypatch.setenv("GOSSIP_YOUNG", "1")
+    monkeypatch.setenv("GOSSIP_YOUNG_CAP", "5")
+    sim = gossip.P2PGossipNetworkSimulation(2000, topo_seed=77, node_seed=78,
+                                            flags=gossip.F_TILE_PER_TICK)
+    sim.CreateRandomTopology(8.0 / 1999, 5.0)
+    st = sim.Start(31.0)
+    assert sim.engine.counters().young_launches > 0
+    ref = oracle.run_reference(num_nodes=2000, connection_prob=8.0 / 1999, sim_time_s=31.0,
+                               topo_seed=77, node_seed=78)
+    for k in STATS:
+        assert np.array_equal(getattr(st, k), getattr(ref, k)), k
+    got = [(gossip.seconds_to_ns(t), g, p, s) for t, g, p, s in sim.periodic]
+    assert got == [tuple(x) for x in ref.periodic]
+
+
+def test_young_off_equals_on(gossip):
+    # 200k nodes (below the auto threshold): forced on == forced off, collisions included
+    n = 200_000
+    topo = gossip.Topology.gnp(n, 16.0 / (n - 1), 79, gossip.TOPO_SKIP, threads=16)
+    t_cut = gossip.seconds_to_ns(5.2)
+    ev = gossip.make_schedule(n, 80, T0, t_cut, id_mask=0xFFFFF)
+    lat = gossip.milliseconds_to_ns(5.0)
+    on = _run(gossip, topo, ev, lat, t_cut, dict(young=1))
+    off = _run(gossip, topo, ev, lat, t_cut, dict(young=0))
+    a, b = on.stats(), off.stats()
+    assert on.counters().young_launches > 0 and off.counters().young_launches == 0
+    for k in STATS:
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    on.close()
+    off.close()
