@@ -112,7 +112,8 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
     slice_tick = SLICE_NS // L_NS
     acc = dict(elapsed=0.0, edges=0, gens=0, launches=0, pull_ms=0.0, moved=0, dense=0, pe=0,
                col=0, nz=0, srd=0, swr=0, fwr=0, words_hw=0, words_cap=0, dev_bytes=0, nt=0,
-               grid=0, ramp_ticks=0)
+               grid=0, ramp_ticks=0, young_ms=0.0, young_launches=0, young_bytes=0, young_sl=0,
+               young_fb=0)
     for s in my_shards:
         t_eng = time.perf_counter()
         eng = gossip.Engine(wl["nodes"], L_NS, T0_NS, T_CUT_NS, device=local, flags=flags,
@@ -147,6 +148,11 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
                      ("col", "pull_col_ids"), ("nz", "pull_nz_reads"), ("srd", "pull_seen_reads"),
                      ("swr", "pull_seen_writes"), ("fwr", "pull_f_writes")):
             acc[k] += getattr(c1, f)
+        acc["young_ms"] += c1.young_ms
+        acc["young_launches"] += c1.young_launches
+        acc["young_bytes"] += c1.young_bytes_moved
+        acc["young_sl"] += c1.young_slot_lines
+        acc["young_fb"] += c1.young_fallback_rows
         acc["words_hw"] = max(acc["words_hw"], c1.words_hw)
         acc["words_cap"] = max(acc["words_cap"], c1.words_cap)
         acc["dev_bytes"] = max(acc["dev_bytes"], c1.device_bytes)
@@ -339,9 +345,27 @@ def main():
                         acc["moved"] - 16 * acc["pe"] - 4 * acc["col"] - 8 * acc["nz"] -
                         16 * (acc["srd"] + acc["swr"] + acc["fwr"])),
                 },
-                "pull_fraction_of_step": (pull_ms_max / (elapsed * 1e3)) if elapsed > 0 else None,
+                "pull_fraction_of_step": ((pull_ms_max + acc["young_ms"]) / (elapsed * 1e3)) if elapsed > 0 else None,
             },
         }
+        if acc["young_launches"]:
+            yl = acc["young_launches"]
+            y_ms = acc["young_ms"] / yl
+            out["roofline"]["young_tiles"] = {
+                "kernel": "k_pull_young",
+                "avg_launch_ms": y_ms,
+                "launches": yl,
+                "bytes_per_launch": acc["young_bytes"] / yl,
+                "achieved": acc["young_bytes"] / yl / (y_ms * 1e6) if y_ms > 0 else None,
+                "slot_lines_per_launch": acc["young_sl"] / yl,
+                "fallback_rows_per_launch": acc["young_fb"] / yl,
+            }
+            tot_ms = avg_ms + acc["young_ms"] / max(launches, 1)
+            tot_b = bytes_per_launch + acc["young_bytes"] / max(launches, 1)
+            out["roofline"]["pull_phase"] = {
+                "kernels": "k_pull + k_pull_young", "ms_per_tick": tot_ms, "bytes_per_tick": tot_b,
+                "achieved": tot_b / (tot_ms * 1e6) if tot_ms > 0 else None,
+                "frac": (tot_b / (tot_ms * 1e6)) / HBM_PEAK_GBS if tot_ms > 0 else None}
         traffic, why = pmc_traffic(wl["name"], out)
         out["roofline"]["traffic"] = traffic
         if why:
