@@ -1184,7 +1184,7 @@ int gossip_engine::tick_step_a(int64_t t) {
     // 3b. young tiles of this tick (young_kernel.h): every tile F_cur holds in slots (it was
     //     write-sparse last tick) plus fresh tiles opened by this tick's births; the youngest of
     //     them stay (or become) write-sparse while their oldest shares are <= young_age hops old.
-    uint32_t ny = 0, nwt = 0;
+    uint32_t ny = 0, nwt = 0, ny_read = 0, ny_leave = 0;
     YoungPack* YP = young ? h_young[slot] : nullptr;
     std::vector<uint8_t> new_widx;
     if (young) {
@@ -1224,9 +1224,19 @@ int gossip_engine::tick_step_a(int64_t t) {
             }
             YP->yt[ny++] = y;
         }
-        std::sort(YP->yt, YP->yt + ny, [](const YoungTile& a, const YoungTile& b) { return a.tile < b.tile; });
-        for (uint32_t i = 0; i < ny; i++)
+        // order (young_kernel.h): leaving tiles, staying read tiles, fresh tiles; each by tile
+        auto part = [](const YoungTile& y) {
+            return (y.flags & YT_READ) ? ((y.flags & YT_WRITE) ? 1 : 0) : 2;
+        };
+        std::sort(YP->yt, YP->yt + ny, [&](const YoungTile& a, const YoungTile& b) {
+            return part(a) != part(b) ? part(a) < part(b) : a.tile < b.tile;
+        });
+        for (uint32_t i = 0; i < ny; i++) {
+            const int pt = part(YP->yt[i]);
+            ny_leave += pt == 0;
+            ny_read += pt <= 1;
             if (YP->yt[i].flags & YT_READ) YP->rmap[YP->yt[i].r_idx] = (uint8_t)i;
+        }
         for (uint32_t q = 0; q < nb; q++) {
             const uint32_t tl = B[q].col >> 10;
             B[q].widx = tl < new_widx.size() ? new_widx[tl] : 0xffu;
@@ -1394,14 +1404,18 @@ int gossip_engine::tick_step_a(int64_t t) {
                 timers.emplace_back(e0, e1);
             }
             if (ny) {  // the young tiles (young_kernel.h), after k_pull wrote the nz words
+                for (uint32_t i = ny_read; i < ny; i++)  // fresh tiles: clear their seen columns
+                    HIP_TRY(hipMemset2DAsync(d_seen + (uint64_t)YP->yt[i].tile * kTileWords, (size_t)stride * 8, 0,
+                                             kTileWords * 8, n, stream));
                 YoungArgs y;
                 y.rowptr = a.rowptr; y.col = a.col; y.deg = d_deg;
                 y.Fcur = d_F[fcur]; y.Fnext = d_F[nxt]; y.seen = d_seen;
                 y.slot_cur = d_slot[fcur]; y.slot_next = d_slot[nxt];
                 y.ctl = d_ctl[slot]; y.wflags = d_wflags[slot];
-                y.recv = d_recv; y.sent = d_sent; y.live = d_live[lv]; y.live_prev = a.live_prev;
+                y.recv = d_recv; y.sent = d_sent; y.live = d_live[lv];
                 y.snap = snap_ptr; y.acct = d_acct; y.nz_next = d_nz[nxt]; y.ntw = ntw;
-                y.yt = d_young[slot]->yt; y.ny = ny; y.rmap = d_young[slot]->rmap;
+                y.yt = d_young[slot]->yt; y.ny = ny; y.nr = ny_read; y.nt = ny_leave;
+                y.rmap = d_young[slot]->rmap;
                 y.n = v1; y.v0 = v0; y.stride = stride;
                 y.cap = (uint32_t)std::min<int64_t>(kSlotU16 - 1, std::max<int64_t>(1, opt_young_cap));
                 const uint32_t yg = (uint32_t)std::max<uint64_t>(
@@ -1412,7 +1426,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                     y1 = get_event();
                     HIP_TRY(hipEventRecord(y0, stream));
                 }
-                k_pull_young<<<yg, 256, young_lds_bytes(ny), stream>>>(y);
+                k_pull_young<<<yg, 256, young_lds_bytes(ny, ny_read), stream>>>(y);
                 HIP_TRY(hipGetLastError());
                 if (cfg.flags & GOSSIP_F_TIMING) {
                     HIP_TRY(hipEventRecord(y1, stream));
