@@ -1404,9 +1404,6 @@ int gossip_engine::tick_step_a(int64_t t) {
                 timers.emplace_back(e0, e1);
             }
             if (ny) {  // the young tiles (young_kernel.h), after k_pull wrote the nz words
-                for (uint32_t i = ny_read; i < ny; i++)  // fresh tiles: clear their seen columns
-                    HIP_TRY(hipMemset2DAsync(d_seen + (uint64_t)YP->yt[i].tile * kTileWords, (size_t)stride * 8, 0,
-                                             kTileWords * 8, n, stream));
                 YoungArgs y;
                 y.rowptr = a.rowptr; y.col = a.col; y.deg = d_deg;
                 y.Fcur = d_F[fcur]; y.Fnext = d_F[nxt]; y.seen = d_seen;

@@ -29,7 +29,7 @@
 // dense rows of the tiles leaving the young set.  The code keeps few registers and ~5 KiB of LDS
 // per wave so that 7-8 waves per SIMD hide the round trips (an explicitly pipelined variant
 // measured no faster: the loop-carried registers forced vmcnt(0) waits, profiles/r02/).
-// Fresh tiles' seen columns are cleared by the host (hipMemset2DAsync), and the young words'
+// Fresh tiles' seen words are cleared here (row by row), and the young words'
 // liveness is reported as all-ones (a young tile is alive by definition; it retires after it
 // leaves the young set, through k_pull's exact liveness).
 #pragma once
@@ -102,7 +102,7 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m, uint32_t l
     return (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-__global__ __launch_bounds__(256, 6) void k_pull_young(YoungArgs a) {
+__global__ __launch_bounds__(256, 5) void k_pull_young(YoungArgs a) {
     extern __shared__ unsigned long long smem[];
     const uint32_t nrw = a.nr * 16u;  // accumulated words
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -229,8 +229,18 @@ __global__ __launch_bounds__(256, 6) void k_pull_young(YoungArgs a) {
                 ntouch += (uint32_t)__popcll(m);
             }
             __builtin_amdgcn_wave_barrier();
-            // ---- dedup against the own seen words ----
+            // ---- dedup against the own seen words (the first 4 x 64 loads issued together) ----
             uint32_t cnt = 0, cnt_sp = 0;
+            uint64_t svq[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const uint32_t t = (uint32_t)r * 64u + lane;
+                svq[r] = 0ull;
+                if (t < ntouch) {
+                    const uint32_t i = s_list[t];
+                    svq[r] = a.seen[v * stride + s_yt[i >> 4].tile * 16u + (i & 15u)];
+                }
+            }
             for (uint32_t t0 = 0; t0 < ntouch; t0 += 64) {
                 const uint32_t t = t0 + lane;
                 const bool valid = t < ntouch;
@@ -241,7 +251,8 @@ __global__ __launch_bounds__(256, 6) void k_pull_young(YoungArgs a) {
                 if (valid) {
                     const uint32_t f = s_wf[i];
                     uint64_t* sp = a.seen + v * stride + w;
-                    const uint64_t sv = *sp;
+                    const uint32_t r = t0 >> 6;
+                    const uint64_t sv = r == 0 ? svq[0] : r == 1 ? svq[1] : r == 2 ? svq[2] : r == 3 ? svq[3] : *sp;
                     const uint64_t keep = (f & WF_KEEP) ? a.ctl[w].keep : ~0ull;
                     x = s_acc[i] & ~sv & keep;
                     if (f & WF_GROUP) x = group_fix(x, sv, a.ctl[w].gmask, a.ctl[w].gstart);
@@ -309,10 +320,16 @@ __global__ __launch_bounds__(256, 6) void k_pull_young(YoungArgs a) {
             // ---- reset the touched accumulator words, counters ----
             for (uint32_t t = lane; t < ntouch; t += 64) s_acc[s_list[t]] = 0ull;
             __builtin_amdgcn_wave_barrier();
+            // fresh write-sparse tiles [nr, ny): clear their seen words (stale from the tiles'
+            // previous use; k_births sets this tick's own-generation bits after this kernel)
+            for (uint32_t q0 = a.nr; q0 < a.ny; q0 += 4) {
+                const uint32_t q = q0 + (lane >> 4);
+                if (q < a.ny) a.seen[v * stride + s_yt[q].tile * 16u + (lane & 15u)] = 0ull;
+            }
             const uint32_t c = (uint32_t)wave_sum((unsigned long long)cnt);
-            if (lane == 0 && c) {
-                a.recv[v] += c;
-                a.sent[v] += (uint64_t)c * a.deg[v];
+            if (lane == 0 && c) {  // no-return atomics: nothing waits on them
+                atomicAdd(&a.recv[v], c);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&a.sent[v]), (unsigned long long)c * a.deg[v]);
             }
         }
     }
