@@ -237,8 +237,8 @@ def main():
     while True:
         shards = passes * world
         my_shards = [rank * passes + q for q in range(passes)]
-        if rehearsal:
-            shards, my_shards = args.rehearse_shards * passes, [0]
+        if rehearsal:  # shard 0 of S (S doubled with passes if it does not fit)
+            shards, my_shards = args.rehearse_shards * (passes // max(1, -(-wl["fit_shards"] // world))), [0]
         err = None
         try:
             acc = run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, flags)

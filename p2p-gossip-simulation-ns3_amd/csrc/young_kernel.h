@@ -102,7 +102,7 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m, uint32_t l
     return (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-__global__ __launch_bounds__(256, 5) void k_pull_young(YoungArgs a) {
+__global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
     extern __shared__ unsigned long long smem[];
     const uint32_t nrw = a.nr * 16u;  // accumulated words
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
