@@ -219,7 +219,10 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *   "young_age"        tiles stay in slots while their oldest shares are <= this many hops (4)
  *                                                                          [GOSSIP_YOUNG_AGE]
  *   "young_cap"        slot entries per node before it falls back to dense rows (1..127)
- *                                                                          [GOSSIP_YOUNG_CAP] */
+ *                                                                          [GOSSIP_YOUNG_CAP]
+ *   "mem_limit"        bytes of device memory the engine may hold, 0 = what the device has
+ *                      free; a window that outgrows it fails with GOSSIP_ECAPACITY / ENOMEM
+ *                      (callers then split the shares into more shards)   [GOSSIP_MEM_LIMIT] */
 int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value);
 /* The mode the engine runs (AUTO resolves at gossip_engine_set_graph). */
 int gossip_engine_mode(const gossip_engine* e);

@@ -551,6 +551,7 @@ struct gossip_engine {
     int64_t opt_young = -1;           // young tiles (k_pull_young): -1 auto, 0 off, 1 on
     int64_t opt_young_age = 4;        // write-sparse while the oldest shares are <= this many hops
     int64_t opt_young_cap = 127;      // slot entries per node before it overflows to dense rows
+    int64_t opt_mem_limit = 0;        // bytes of device memory the engine may hold (0: the device's)
     uint32_t last_nt = 0, last_grid = 0;  // variant of the last pull launch (counters)
     // ---- young tiles (young_kernel.h)
     bool young = false;
@@ -818,6 +819,11 @@ int gossip_engine::alloc_device() {
     const uint64_t slot_bytes = young ? 2ull * n * kSlotU16 * 2u : 0ull;
     size_t freeb = 0, totalb = 0;
     HIP_TRY(hipMemGetInfo(&freeb, &totalb));
+    if (opt_mem_limit > 0) {  // a memory budget below the device's (tests, co-located engines)
+        const uint64_t graph = (uint64_t)n * 4 + nnz * 4 + ((uint64_t)n + 1) * 8;
+        const uint64_t lim = (uint64_t)opt_mem_limit > graph ? (uint64_t)opt_mem_limit - graph : 0ull;
+        freeb = (size_t)std::min<uint64_t>(freeb, lim);
+    }
     if (cfg.max_words == 0 && row_count == 1) {
         // (row-partitioned ranks skip this: their strides must agree for the row exchange)
         // Headroom over the estimate: up to +25% (at least 2 tiles) of row capacity, as far as
@@ -932,6 +938,7 @@ int gossip_engine::grow(uint32_t new_stride) {
     size_t freeb = 0, totalb = 0;
     HIP_TRY(hipMemGetInfo(&freeb, &totalb));
     int ok = nb + (64ull << 20) <= (uint64_t)freeb ? 1 : 0;
+    if (opt_mem_limit > 0 && device_bytes + 3 * (nb - (uint64_t)n * stride * 8) > (uint64_t)opt_mem_limit) ok = 0;
     if (comm) {
         // Row-partitioned ranks widen in lockstep (their strides must agree for the exchange):
         // all of them grow or all fail, never one rank alone while the others wait in the next
@@ -1642,6 +1649,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_young = env_option("GOSSIP_YOUNG", -1);
         e->opt_young_age = env_option("GOSSIP_YOUNG_AGE", 4);
         e->opt_young_cap = env_option("GOSSIP_YOUNG_CAP", 127);
+        e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
         e->dense = cfg->mode == GOSSIP_MODE_DENSE;
         e->handshake = (cfg->flags & GOSSIP_F_HANDSHAKE) != 0;
@@ -1906,6 +1914,10 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     } else if (k == "young_cap") {
         if (value < 1 || value > (int64_t)kSlotU16 - 1) return set_error(GOSSIP_EINVAL, "young_cap: 1 .. 127 entries");
         e->opt_young_cap = value;
+    } else if (k == "mem_limit") {
+        if (value < 0) return set_error(GOSSIP_EINVAL, "mem_limit >= 0 bytes");
+        if (e->have_sched) return set_error(GOSSIP_ESTATE, "mem_limit: set before the schedule");
+        e->opt_mem_limit = value;
     } else if (k == "dense_min_tiles") {
         if (value < 1) return set_error(GOSSIP_EINVAL, "dense_min_tiles >= 1");
         e->opt_dense_min_tiles = value;

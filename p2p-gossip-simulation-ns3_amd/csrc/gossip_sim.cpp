@@ -8,13 +8,21 @@
 // syntax --name=value; "--name value" is accepted too).  std::random_device is replaced by
 // explicit seeds (--seed for the topology, --nodeSeed for the per-node share RNGs), printed
 // so that a run can be reproduced.  The report is the reference's NS_LOG_INFO text.
+//
+// Multi-GPU (--gpus=N, one host thread per device): --layout=shards (default) runs the share
+// instances in S >= N independent shards (gossip_shard_events; no exchange, counters summed on
+// the host), doubling S on its own when a shard's live window does not fit a device
+// (GOSSIP_ECAPACITY / GOSSIP_ENOMEM); --layout=rows runs the north star's row partition, one
+// rank per device, with the per-tick frontier exchange over RCCL (gossip_engine_connect_rccl).
 #include <cerrno>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gossip.h"
@@ -41,6 +49,10 @@ struct Options {
     std::string mode = "auto";         // auto | csr | dense
     std::string dumpLinks, dumpEvents, linksIn, eventsIn, dumpTrace, netanim;
     std::string log;  // per-event NS_LOG_INFO lines ("-" = stderr, where NS_LOG writes)
+    int gpus = 1;                      // devices device .. device+gpus-1, one thread each
+    uint32_t shards = 0;               // share shards (0: gpus); doubled on capacity errors
+    std::string layout = "shards";     // shards | rows
+    double memLimitMB = 0;             // device memory budget per engine (0: the device's)
 };
 
 void usage() {
@@ -52,7 +64,8 @@ void usage() {
                  "                  [--noPeriodic] [--timing] [--handshake] [--hopBatch] [--linkTiming]\n"
                  "                  [--mode=auto|csr|dense] [--dumpLinks=F] [--dumpEvents=F]\n"
                  "                  [--links=F] [--events=F] [--dumpTrace=F] [--netanim=F]\n"
-                 "                  [--log=F|-]\n");
+                 "                  [--log=F|-] [--gpus=N] [--shards=S] [--layout=shards|rows]\n"
+                 "                  [--memLimitMB=M]\n");
 }
 
 bool parse(int argc, char** argv, Options& o) {
@@ -115,6 +128,10 @@ bool parse(int argc, char** argv, Options& o) {
         else if (key == "dumpTrace") { if (!need()) return false; o.dumpTrace = val; }
         else if (key == "log") { if (!need()) return false; o.log = val; }
         else if (key == "netanim") { if (!need()) return false; o.netanim = val; }
+        else if (key == "gpus") { if (!num(d) || d < 1 || d > 64) return false; o.gpus = (int)d; }
+        else if (key == "shards") { if (!num(d) || d < 0 || d > 4096) return false; o.shards = (uint32_t)d; }
+        else if (key == "layout") { if (!need()) return false; o.layout = val; }
+        else if (key == "memLimitMB") { if (!num(o.memLimitMB) || o.memLimitMB < 0) return false; }
         else {
             std::fprintf(stderr, "unknown option --%s\n", key.c_str());
             return false;
@@ -154,6 +171,79 @@ bool write_netanim(const std::string& path, uint32_t n, const std::vector<uint32
 int die(const char* what) {
     std::fprintf(stderr, "gossip_sim: %s failed: %s\n", what, gossip_last_error());
     return 1;
+}
+
+// What every engine of a run contributes (summed over shards / row ranks on the host).
+struct Part {
+    std::vector<uint32_t> gen, recv, fwd, proc, peers, sock;
+    std::vector<uint64_t> sent;
+    std::vector<int64_t> snap_t;
+    std::vector<uint64_t> snap_gen, snap_proc;
+    std::vector<uint32_t> tn, ti, th;
+    std::vector<int64_t> tt;
+    std::vector<uint8_t> tv;
+    gossip_counters c{};
+    int64_t first_tick = 0, end_tick = 0;
+    int rc = 0;
+    std::string err;
+};
+
+// One engine, start to finish: shard `rank` of `count` (share sharding) or row rank `rank` of
+// `count` (layout rows, exchange over RCCL with the shared communicator id `uid`).
+void run_engine(const gossip_config& base, int device, bool rows, uint32_t rank, uint32_t count,
+                const uint8_t* uid, const gossip_topology* topo, const gossip_schedule* sched,
+                const std::vector<double>& per_t, bool link_timing, bool want_trace, double mem_limit_mb,
+                Part& out) {
+    gossip_config cfg = base;
+    cfg.device = device;
+    if (!rows && count > 1) {
+        cfg.shard_rank = rank;
+        cfg.shard_count = count;
+    }
+    gossip_engine* eng = nullptr;
+    auto fail = [&](const char* what, int rc) {
+        out.rc = rc;
+        out.err = std::string(what) + ": " + gossip_last_error();
+        if (eng) gossip_engine_destroy(eng);
+    };
+    int rc = gossip_engine_create(&cfg, &eng);
+    if (rc) return fail("engine create", rc);
+    if (rows && count > 1 && (rc = gossip_engine_set_row_partition(eng, rank, count))) return fail("row partition", rc);
+    if (mem_limit_mb > 0 && (rc = gossip_engine_set_option(eng, "mem_limit", (int64_t)(mem_limit_mb * 1048576.0))))
+        return fail("mem limit", rc);
+    if ((rc = gossip_engine_set_topology(eng, topo))) return fail("engine graph", rc);
+    // NS-3 link timing: 5 Mbps DataRate (p2pnetwork.cc:113) = 1600 ns/byte, 54 header bytes
+    // (PPP + IPv4 + TCP with timestamps), 1 ns TcpSocketBase send deferral (gossip.h)
+    if (link_timing && (rc = gossip_engine_set_link_timing(eng, 1600, 54, 1))) return fail("link timing", rc);
+    for (double t : per_t)  // Start(): p2pnetwork.cc:201-204
+        if ((rc = gossip_engine_add_snapshot(eng, gossip_seconds_to_ns(t)))) return fail("snapshot", rc);
+    if ((rc = gossip_engine_set_schedule_obj(eng, sched))) return fail("engine schedule", rc);
+    if (rows && count > 1 && (rc = gossip_engine_connect_rccl(eng, uid, 128))) return fail("rccl connect", rc);
+    out.first_tick = gossip_engine_first_tick(eng);
+    out.end_tick = gossip_engine_end_tick(eng);
+    if ((rc = gossip_engine_run(eng, gossip_engine_end_tick(eng)))) return fail("engine run", rc);
+    if ((rc = gossip_engine_sync(eng))) return fail("engine sync", rc);
+    const uint32_t n = base.num_nodes;
+    out.gen.assign(n, 0); out.recv.assign(n, 0); out.fwd.assign(n, 0); out.proc.assign(n, 0);
+    out.peers.assign(n, 0); out.sock.assign(n, 0); out.sent.assign(n, 0);
+    if ((rc = gossip_engine_get_stats(eng, out.gen.data(), out.recv.data(), out.fwd.data(), out.sent.data(),
+                                      out.proc.data(), out.peers.data(), out.sock.data())))
+        return fail("stats", rc);
+    for (size_t k = 0; k < per_t.size(); k++) {
+        int64_t tns;
+        uint64_t tg, tp;
+        if ((rc = gossip_engine_get_snapshot(eng, (uint32_t)k, &tns, &tg, &tp))) return fail("snapshot read", rc);
+        out.snap_t.push_back(tns);
+        out.snap_gen.push_back(tg);
+        out.snap_proc.push_back(tp);
+    }
+    const uint64_t m = want_trace ? gossip_engine_trace_size(eng) : 0;
+    out.tn.resize(m); out.ti.resize(m); out.th.resize(m); out.tt.resize(m); out.tv.resize(m);
+    if (m && (rc = gossip_engine_get_trace(eng, out.tn.data(), out.ti.data(), out.tt.data(), out.th.data(),
+                                           out.tv.data())))
+        return fail("trace", rc);
+    gossip_engine_get_counters(eng, &out.c);
+    gossip_engine_destroy(eng);
 }
 
 }  // namespace
@@ -227,7 +317,7 @@ int main(int argc, char** argv) {
         if (f) std::fclose(f);
     }
 
-    // ---- engine ----
+    // ---- engines (one per shard / row rank; one host thread per device) ----
     gossip_config cfg{};
     cfg.num_nodes = n;
     cfg.latency_ns = L;
@@ -238,51 +328,80 @@ int main(int argc, char** argv) {
     else if (o.mode == "dense") cfg.mode = GOSSIP_MODE_DENSE;
     else if (o.mode == "auto") cfg.mode = GOSSIP_MODE_AUTO;
     else { usage(); return 2; }
+    if (o.layout != "shards" && o.layout != "rows") { usage(); return 2; }
+    const bool rows = o.layout == "rows";
     cfg.max_words = o.maxWords;
+    const bool want_trace = !(o.dumpTrace.empty() && o.log.empty());
     cfg.flags = (o.timing ? GOSSIP_F_TIMING : 0u) | (o.handshake ? GOSSIP_F_HANDSHAKE : 0u) |
-                (o.hopBatch ? GOSSIP_F_HOP_BATCH : 0u) | (o.dumpTrace.empty() && o.log.empty() ? 0u : GOSSIP_F_TRACE);
+                (o.hopBatch ? GOSSIP_F_HOP_BATCH : 0u) | (want_trace ? GOSSIP_F_TRACE : 0u);
     if (!o.log.empty() && o.handshake) {
         std::fprintf(stderr, "gossip_sim: --log renders the ideal / --linkTiming models, not --handshake\n");
         return 2;
     }
-    gossip_engine* eng = nullptr;
-    if (gossip_engine_create(&cfg, &eng)) return die("engine create");
-    if (gossip_engine_set_topology(eng, topo)) return die("engine graph");
-    // NS-3 link timing: 5 Mbps DataRate (p2pnetwork.cc:113) = 1600 ns/byte, 54 header bytes
-    // (PPP + IPv4 + TCP with timestamps), 1 ns TcpSocketBase send deferral (gossip.h)
-    if (o.linkTiming && gossip_engine_set_link_timing(eng, 1600, 54, 1)) return die("link timing");
     std::vector<double> per_t;
     if (o.periodic)
-        for (double t = 10.0; t < o.simTime; t += 10.0) {  // Start(): p2pnetwork.cc:201-204
-            if (gossip_engine_add_snapshot(eng, gossip_seconds_to_ns(t))) return die("snapshot");
-            per_t.push_back(t);
-        }
-    if (gossip_engine_set_schedule_obj(eng, sched)) return die("engine schedule");
+        for (double t = 10.0; t < o.simTime; t += 10.0) per_t.push_back(t);  // p2pnetwork.cc:201-204
 
     std::printf("Starting gossip network simulation for %g seconds\n", o.simTime);
+    uint32_t count = rows ? (uint32_t)o.gpus : std::max<uint32_t>(o.shards ? o.shards : 1u, (uint32_t)o.gpus);
+    std::vector<Part> parts;
+    double wall = 0.0;
+    for (;;) {
+        parts.assign(count, Part{});
+        std::vector<uint8_t> uid(128, 0);
+        if (rows && count > 1 && gossip_rccl_unique_id(uid.data(), 128)) return die("rccl unique id");
+        auto w0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> th;
+        const uint32_t ng = (uint32_t)o.gpus;
+        for (uint32_t g = 0; g < std::min(ng, count); g++)
+            th.emplace_back([&, g] {
+                // device g runs shards g, g + N, ... (rows: exactly rank g)
+                for (uint32_t r = g; r < count; r += ng)
+                    run_engine(cfg, o.device + (int)g, rows, r, count, uid.data(), topo, sched, per_t,
+                               o.linkTiming, want_trace, o.memLimitMB, parts[r]);
+            });
+        for (auto& t : th) t.join();
+        wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
+        int worst = 0;
+        std::string err;
+        for (const Part& p : parts)
+            if (p.rc) { worst = p.rc; err = p.err; }
+        if (!worst) break;
+        if (!rows && (worst == GOSSIP_ECAPACITY || worst == GOSSIP_ENOMEM) && count < 4096) {
+            std::fprintf(stderr, "gossip_sim: %u share shard(s) do not fit (%s); retrying with %u\n", count,
+                         err.c_str(), 2 * count);
+            count *= 2;
+            continue;
+        }
+        std::fprintf(stderr, "gossip_sim: %s\n", err.c_str());
+        return 1;
+    }
     if (o.hopBatch)
         std::printf("seeds: topology %u, nodes %u; latency %lld ns; hop-batched from tick %lld\n", o.seed,
-                    o.nodeSeed, (long long)L, (long long)gossip_engine_first_tick(eng));
+                    o.nodeSeed, (long long)L, (long long)parts[0].first_tick);
     else
         std::printf("seeds: topology %u, nodes %u; latency %lld ns; ticks [%lld, %lld)\n", o.seed,
-                    o.nodeSeed, (long long)L, (long long)gossip_engine_first_tick(eng),
-                    (long long)gossip_engine_end_tick(eng));
-    auto w0 = std::chrono::steady_clock::now();
-    if (gossip_engine_run(eng, gossip_engine_end_tick(eng))) return die("engine run");
-    if (gossip_engine_sync(eng)) return die("engine sync");
-    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
-
-    std::vector<uint32_t> gen(n), recv(n), fwd(n), proc(n), peers(n), sock(n);
-    std::vector<uint64_t> sent(n);
-    if (gossip_engine_get_stats(eng, gen.data(), recv.data(), fwd.data(), sent.data(), proc.data(),
-                                peers.data(), sock.data()))
-        return die("stats");
+                    o.nodeSeed, (long long)L, (long long)parts[0].first_tick, (long long)parts[0].end_tick);
+    if (count > 1)
+        std::printf("engines: %u %s on %d GPU(s)\n", count, rows ? "row ranks (RCCL exchange)" : "share shards",
+                    o.gpus);
+    std::vector<uint32_t> gen(n, 0), recv(n, 0), fwd(n, 0), proc(n, 0), peers = parts[0].peers, sock = parts[0].sock;
+    std::vector<uint64_t> sent(n, 0);
+    for (const Part& p : parts)  // counters add exactly over shards and row ranks
+        for (uint32_t v = 0; v < n; v++) {
+            gen[v] += p.gen[v]; recv[v] += p.recv[v]; fwd[v] += p.fwd[v]; proc[v] += p.proc[v];
+            sent[v] += p.sent[v];
+        }
     uint64_t total_sock = 0;
     for (uint32_t v = 0; v < n; v++) total_sock += sock[v];
     for (size_t k = 0; k < per_t.size(); k++) {
-        int64_t tns;
-        uint64_t tg, tp;
-        if (gossip_engine_get_snapshot(eng, (uint32_t)k, &tns, &tg, &tp)) return die("snapshot read");
+        const int64_t tns = parts[0].snap_t[k];
+        uint64_t tg = 0, tp = 0;
+        for (const Part& p : parts) {
+            // row ranks report the global generation total each; shards their own
+            tg = rows ? p.snap_gen[k] : tg + p.snap_gen[k];
+            tp += p.snap_proc[k];
+        }
         // sockets exist from makeconnections (t_start) until StopAllNodes (t_cut)
         const uint64_t sockets_now = (tns >= t_start && tns <= t_cut) ? total_sock : 0;
         std::string buf((size_t)gossip_format_periodic(per_t[k], n, tg, tp, sockets_now, nullptr, 0) + 1, '\0');
@@ -309,12 +428,17 @@ int main(int argc, char** argv) {
         std::fputs(buf.c_str(), stdout);
     }
     std::printf("All nodes stopped.\n");
-    const uint64_t m_tr = o.dumpTrace.empty() && o.log.empty() ? 0 : gossip_engine_trace_size(eng);
-    std::vector<uint32_t> tn(m_tr), ti(m_tr), th(m_tr);
-    std::vector<int64_t> tt(m_tr);
-    std::vector<uint8_t> tv(m_tr);
-    if (m_tr && gossip_engine_get_trace(eng, tn.data(), ti.data(), tt.data(), th.data(), tv.data()))
-        return die("trace");
+    std::vector<uint32_t> tn, ti, th;
+    std::vector<int64_t> tt;
+    std::vector<uint8_t> tv;
+    for (const Part& p : parts) {  // every first contact happened on exactly one engine
+        tn.insert(tn.end(), p.tn.begin(), p.tn.end());
+        ti.insert(ti.end(), p.ti.begin(), p.ti.end());
+        th.insert(th.end(), p.th.begin(), p.th.end());
+        tt.insert(tt.end(), p.tt.begin(), p.tt.end());
+        tv.insert(tv.end(), p.tv.begin(), p.tv.end());
+    }
+    const uint64_t m_tr = tn.size();
     if (!o.log.empty()) {  // NS_LOG_INFO lines of the gossip path, rendered from the trace
         std::vector<gossip_gen_event> ev(gossip_schedule_size(sched));
         if (!ev.empty()) gossip_schedule_get(sched, ev.data());
@@ -341,7 +465,15 @@ int main(int argc, char** argv) {
         std::fclose(f);
     }
     gossip_counters c{};
-    gossip_engine_get_counters(eng, &c);
+    for (const Part& p : parts) {
+        c.ticks = std::max(c.ticks, p.c.ticks);
+        c.edge_events += p.c.edge_events;
+        c.pull_ms += p.c.pull_ms;
+        c.pull_launches += p.c.pull_launches;
+        c.pull_bytes += p.c.pull_bytes;
+        c.words_hw = std::max(c.words_hw, p.c.words_hw);
+        c.words_cap = std::max(c.words_cap, p.c.words_cap);
+    }
     std::fprintf(stderr,
                  "[engine] %llu ticks, %llu edge events in %.3f s wall (%.3e edge events/s), "
                  "window %u/%u words%s\n",
@@ -351,7 +483,6 @@ int main(int argc, char** argv) {
     if (o.timing && c.pull_ms > 0)
         std::fprintf(stderr, "[engine] pull kernel %.3f ms over %llu launches, %.1f GB/s algorithmic\n",
                      c.pull_ms, (unsigned long long)c.pull_launches, c.pull_bytes / (c.pull_ms * 1e6));
-    gossip_engine_destroy(eng);
     gossip_schedule_destroy(sched);
     gossip_topology_destroy(topo);
     return 0;

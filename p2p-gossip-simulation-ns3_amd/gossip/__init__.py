@@ -499,7 +499,7 @@ class P2PGossipNetworkSimulation:
 
     def __init__(self, numNodes: int, topo_seed: int = 1, node_seed: int = 1000, device: int = 0,
                  topology_kind: int | None = None, threads: int = 8, flags: int = 0,
-                 link_timing=None):
+                 link_timing=None, shards: int = 1, options=None):
         if numNodes < 2:
             # p2pnetwork.cc:82 calls nodes.Get(1) for the fix-up of row 0: out of range.
             raise GossipError("numNodes < 2: the reference's topology fix-up aborts")
@@ -511,6 +511,8 @@ class P2PGossipNetworkSimulation:
         self.threads = threads
         self.flags = flags
         self.link_timing = link_timing  # e.g. LINK_5MBPS (needs flags |= F_HOP_BATCH)
+        self.shards = shards            # share shards run one after another on `device`
+        self.options = dict(options or {})  # gossip_engine_set_option name -> value
         self.topology = None
         self.latency_ns = None
         self.engine = None
@@ -525,38 +527,72 @@ class P2PGossipNetworkSimulation:
                                      self.threads)
         self.latency_ns = milliseconds_to_ns(latency)
 
-    def Start(self, simulationTime: float = 100.0, statsInterval: float = 10.0):
+    def _run_shard(self, ev, t_start, t_cut, snaps, rank, count):
+        eng = Engine(self.numNodes, self.latency_ns, t_start, t_cut, device=self.device,
+                     flags=self.flags, shard_rank=rank, shard_count=count)
+        for k, v in self.options.items():
+            eng.set_option(k, v)
+        eng.set_topology(self.topology)
+        if self.link_timing:
+            eng.set_link_timing(*self.link_timing)
+        for t in snaps:
+            eng.add_snapshot(seconds_to_ns(t))
+        eng.set_schedule(ev)
+        eng.run()
+        eng.sync()
+        return eng
+
+    def Start(self, simulationTime: float = 100.0, statsInterval: float = 10.0, events=None):
+        """Run the simulation (p2pnetwork.cc:193-218).  The share instances run as `shards`
+        engines one after another (counters add exactly); when an engine's live window does not
+        fit the device (GOSSIP_ECAPACITY / GOSSIP_ENOMEM) the shard count doubles and the run
+        restarts.  `events` (GEN_EVENT_DTYPE) replays a given schedule instead of the reference's
+        (e.g. one dumped from an NS-3 run)."""
         if self.topology is None:
             raise GossipError("CreateRandomTopology first")
         t_start = seconds_to_ns(5.0)
         t_cut = seconds_to_ns(simulationTime - 0.1)
-        ev = make_schedule(self.numNodes, self.node_seed, t_start, t_cut, threads=self.threads)
-        eng = Engine(self.numNodes, self.latency_ns, t_start, t_cut, device=self.device,
-                     flags=self.flags)
-        eng.set_topology(self.topology)
-        if self.link_timing:
-            eng.set_link_timing(*self.link_timing)
+        ev = (make_schedule(self.numNodes, self.node_seed, t_start, t_cut, threads=self.threads)
+              if events is None else np.ascontiguousarray(events, GEN_EVENT_DTYPE))
         times = []
         t = statsInterval
         while t < simulationTime:
             times.append(t)
-            eng.add_snapshot(seconds_to_ns(t))
             t += statsInterval
-        eng.set_schedule(ev)
-        eng.run()
-        eng.sync()
+        count = max(1, int(self.shards))
+        while True:
+            try:
+                parts = []
+                for r in range(count):
+                    eng = self._run_shard(ev, t_start, t_cut, times, r, count)
+                    parts.append((eng.stats(), [eng.snapshot(k) for k in range(len(times))]))
+                    if r + 1 < count:
+                        eng.close()  # keep only the last engine (counters, trace) alive
+                break
+            except GossipError as e:
+                if e.code not in (E_CAPACITY, E_NOMEM) or count >= 4096:
+                    raise
+                count *= 2
+        self.shards_used = count
         self.engine = eng
-        self.stats = eng.stats()
+        st = parts[0][0]
+        if count > 1:  # counters add exactly over share shards
+            st = Stats(*(sum(getattr(p[0], k).astype(np.uint64) for p in parts).astype(getattr(st, k).dtype)
+                         if k not in ("peers", "sockets") else getattr(st, k)
+                         for k in ("gen", "recv", "fwd", "sent", "processed", "peers", "sockets")))
+        self.stats = st
         if t_cut < t_start:
             self.stats.peers[:] = 0
             self.stats.sockets[:] = 0
         total_sock = int(self.topology.degrees()[1].sum())
         self.periodic = []
         for k, ts in enumerate(times):
-            tns, g, p = eng.snapshot(k)
+            tns = parts[0][1][k][0]
+            g = sum(p[1][k][1] for p in parts)
+            pr = sum(p[1][k][2] for p in parts)
             # sockets exist from makeconnections (t_start) until StopAllNodes (t_cut)
             live = t_start <= tns <= t_cut
-            self.periodic.append((ts, g, p, total_sock if live else 0))
+            self.periodic.append((ts, g, pr, total_sock if live else 0))
         return self.stats
 
     def PrintPeriodicStats(self) -> str:
