@@ -216,7 +216,7 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *   "dense_min_tiles"  MFMA block tiles the K split aims for (512)  [GOSSIP_DENSE_MIN_TILES]
  *   "young"            young-tile slots (k_pull_young): -1 auto (CSR tick engine, n >= 2^20),
  *                      0 off, 1 on (before the schedule)                    [GOSSIP_YOUNG]
- *   "young_age"        tiles stay in slots while their oldest shares are <= this many hops (4)
+ *   "young_age"        tiles stay in slots while their oldest shares are <= this many hops (5)
  *                                                                          [GOSSIP_YOUNG_AGE]
  *   "young_cap"        slot entries per node before it falls back to dense rows (1..127)
  *                                                                          [GOSSIP_YOUNG_CAP]

@@ -549,7 +549,7 @@ struct gossip_engine {
     int64_t opt_pull_lpw = 0;         // 0 = 32 word-lanes for wide windows
     int64_t opt_dense_min_tiles = 512;  // block tiles the MFMA K split aims for
     int64_t opt_young = -1;           // young tiles (k_pull_young): -1 auto, 0 off, 1 on
-    int64_t opt_young_age = 4;        // write-sparse while the oldest shares are <= this many hops
+    int64_t opt_young_age = 5;        // write-sparse while the oldest shares are <= this many hops
     int64_t opt_young_cap = 127;      // slot entries per node before it overflows to dense rows
     int64_t opt_mem_limit = 0;        // bytes of device memory the engine may hold (0: the device's)
     uint32_t last_nt = 0, last_grid = 0;  // variant of the last pull launch (counters)
@@ -1647,7 +1647,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_pull_lpw = env_option("GOSSIP_PULL_LPW", 0);
         e->opt_dense_min_tiles = env_option("GOSSIP_DENSE_MIN_TILES", 512);
         e->opt_young = env_option("GOSSIP_YOUNG", -1);
-        e->opt_young_age = env_option("GOSSIP_YOUNG_AGE", 4);
+        e->opt_young_age = env_option("GOSSIP_YOUNG_AGE", 5);
         e->opt_young_cap = env_option("GOSSIP_YOUNG_CAP", 127);
         e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
