@@ -78,8 +78,9 @@ struct YoungArgs {
 };
 
 __host__ __device__ constexpr size_t young_lds_bytes(uint32_t ny, uint32_t nr) {
-    // 4 waves x (accumulator 8 B + touched list 2 B per read word), tiles, read-word flags, rmap
-    return (size_t)nr * 16u * 10u * 4u + (size_t)ny * sizeof(YoungTile) + (size_t)nr * 16u + 64u;
+    // 4 waves x (accumulator 8 B + touched list 2 B per read word + a slot staging buffer),
+    // tiles, read-word flags, rmap
+    return (size_t)nr * 16u * 10u * 4u + 4u * kSlotU16 * 2u + (size_t)ny * sizeof(YoungTile) + (size_t)nr * 16u + 64u;
 }
 
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane) {
@@ -108,7 +109,8 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     unsigned long long* s_acc = smem + wv * nrw;
     uint16_t* s_list = reinterpret_cast<uint16_t*>(smem + 4u * nrw) + wv * nrw;
-    YoungTile* s_yt = reinterpret_cast<YoungTile*>(reinterpret_cast<uint16_t*>(smem + 4u * nrw) + 4u * nrw);
+    uint16_t* s_out = reinterpret_cast<uint16_t*>(smem + 4u * nrw) + 4u * nrw + wv * kSlotU16;  // 16-B aligned
+    YoungTile* s_yt = reinterpret_cast<YoungTile*>(reinterpret_cast<uint16_t*>(smem + 4u * nrw) + 4u * nrw + 4u * kSlotU16);
     uint8_t* s_wf = reinterpret_cast<uint8_t*>(s_yt + a.ny);
     uint8_t* s_rmap = s_wf + nrw;
     for (uint32_t i = threadIdx.x; i < a.ny; i += 256) s_yt[i] = a.yt[i];
@@ -138,74 +140,61 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
         const uint32_t cnt_nodes = (uint32_t)min<uint64_t>(64u, a.n - c0);
         const int64_t rp = a.rowptr[c0 + min(lane, cnt_nodes)];
         const int64_t rp_end = a.rowptr[c0 + cnt_nodes];
+        // peer ids of node j (lane p = peer p of its first 64), one node ahead of the gather
+        auto load_ids = [&](uint32_t j) -> uint32_t {
+            const int32_t b = __shfl((int)rp, (int)(j & 63u), 64);
+            const int32_t nx = __shfl((int)rp, (int)((j + 1u) & 63u), 64);
+            const int32_t e = j + 1u < 64u ? nx : (int32_t)rp_end;
+            return j < cnt_nodes && (int32_t)lane < e - b ? (uint32_t)a.col[b + (int32_t)lane] : 0xffffffffu;
+        };
+        uint32_t cid_cur = load_ids(0u);
         for (uint32_t jn = 0; jn < cnt_nodes; jn++) {
             const uint64_t v = c0 + jn;
             const int32_t beg = __shfl((int)rp, (int)jn, 64);
             const int32_t nx = __shfl((int)rp, (int)((jn + 1u) & 63u), 64);
             const int32_t end = jn + 1u < 64u ? nx : (int32_t)rp_end;
-            // ---- gather: peers' slots -> accumulator ----
+            const uint32_t cid_next = load_ids(jn + 1u);
+            // ---- gather: peers' whole slots (both lines) -> accumulator ----
             for (int32_t cb = beg; cb < end; cb += 64) {
                 const int32_t np = min(64, end - cb);
-                const uint32_t cid = (int32_t)lane < np ? (uint32_t)a.col[cb + (int32_t)lane] : 0xffffffffu;
+                const uint32_t cid = cb == beg ? cid_cur
+                                               : ((int32_t)lane < np ? (uint32_t)a.col[cb + (int32_t)lane] : 0xffffffffu);
                 t_col += (uint32_t)np;
-                unsigned long long need2 = 0ull, ovf = 0ull;  // bit p: peer cb+p
+                unsigned long long ovf = 0ull;  // bit p: peer cb+p
                 for (int32_t pb = 0; pb < np; pb += 8 * kYoungQ) {
-                    ulonglong2 q[kYoungQ];
+                    ulonglong2 q[kYoungQ], q2[kYoungQ];
 #pragma unroll
                     for (int k = 0; k < kYoungQ; k++) {
                         const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
                         const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64);
-                        q[k] = make_ulonglong2(0ull, 0ull);
-                        if (p < 64u && u != 0xffffffffu)
-                            q[k] = *reinterpret_cast<const ulonglong2*>(a.slot_cur + (uint64_t)u * kSlotU16 + (lane & 7u) * 8u);
+                        q[k] = q2[k] = make_ulonglong2(0ull, 0ull);
+                        if (p < 64u && u != 0xffffffffu) {
+                            const uint16_t* sl = a.slot_cur + (uint64_t)u * kSlotU16 + (lane & 7u) * 8u;
+                            q[k] = *reinterpret_cast<const ulonglong2*>(sl);
+                            q2[k] = *reinterpret_cast<const ulonglong2*>(sl + 64u);
+                        }
                     }
 #pragma unroll
                     for (int k = 0; k < kYoungQ; k++) {
                         const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
                         const bool valid = p < 64u && (uint32_t)__shfl((int)cid, (int)(p & 63u), 64) != 0xffffffffu;
                         const uint32_t hdr = (uint32_t)__shfl((int)(q[k].x & 0xffffull), (int)(lane & ~7u), 64);
-                        t_sl += wave_count(valid && (lane & 7u) == 0u);
+                        t_sl += wave_count(valid && (lane & 7u) == 0u) * 2u;
                         if (valid && hdr != kSlotOverflow) {
-                            const uint32_t lim = min(hdr, 63u);
 #pragma unroll
                             for (int j = 0; j < 8; j++) {
                                 const uint32_t pos = (lane & 7u) * 8u + (uint32_t)j;
-                                if (pos >= 1u && pos <= lim) scatter(slot_entry(q[k], j));
+                                if (pos >= 1u && pos <= hdr) scatter(slot_entry(q[k], j));
+                                if (64u + pos <= hdr) scatter(slot_entry(q2[k], j));
                             }
                         }
-                        const bool lead = (lane & 7u) == 0u && valid;
-                        const unsigned long long m2 = __ballot(lead && hdr != kSlotOverflow && hdr > 63u);
-                        const unsigned long long mo = __ballot(lead && hdr == kSlotOverflow);
-                        // lane 8g leads peer pb + 8k + g: spread the lead bits to peer bits
+                        const unsigned long long mo = __ballot((lane & 7u) == 0u && valid && hdr == kSlotOverflow);
+                        if (mo) {
 #pragma unroll
-                        for (int g = 0; g < 8; g++) {
-                            const uint32_t pp = (uint32_t)pb + (uint32_t)k * 8u + (uint32_t)g;
-                            if (pp < 64u) {
-                                if ((m2 >> (8 * g)) & 1ull) need2 |= 1ull << pp;
-                                if ((mo >> (8 * g)) & 1ull) ovf |= 1ull << pp;
-                            }
+                            for (int g = 0; g < 8; g++)
+                                if ((mo >> (8 * g)) & 1ull) ovf |= 1ull << (((uint32_t)pb + (uint32_t)k * 8u + (uint32_t)g) & 63u);
                         }
                     }
-                }
-                // second lines (entries 64..127) of up to 8 peers per load, 8 lanes each
-                while (need2) {
-                    const uint32_t g = lane >> 3;
-                    unsigned long long m = need2;
-                    for (uint32_t r = 0; r < g && m; r++) m &= m - 1ull;  // g-th set bit
-                    const int p = m ? __builtin_ctzll(m) : -1;
-                    const uint32_t u = (uint32_t)__shfl((int)cid, p < 0 ? 0 : p, 64);
-                    ulonglong2 x = make_ulonglong2(0ull, 0ull);
-                    uint32_t hdr = 0;
-                    if (p >= 0) {
-                        const uint16_t* sl = a.slot_cur + (uint64_t)u * kSlotU16;
-                        x = *reinterpret_cast<const ulonglong2*>(sl + 64u + (lane & 7u) * 8u);
-                        hdr = sl[0];
-                    }
-                    t_sl += min(8u, (uint32_t)__popcll(need2));
-#pragma unroll
-                    for (int j = 0; j < 8; j++)
-                        if (p >= 0 && 64u + (lane & 7u) * 8u + (uint32_t)j <= hdr) scatter(slot_entry(x, j));
-                    for (int r = 0; r < 8 && need2; r++) need2 &= need2 - 1ull;
                 }
                 while (ovf) {  // overflowed peers: their dense rows of every read-sparse tile
                     const int p = __builtin_ctzll(ovf);
@@ -266,10 +255,12 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
                 t_swr += wave_count(x != 0ull);
             }
             __builtin_amdgcn_wave_barrier();
+            cid_cur = cid_next;  // (arrived long ago: the wait here is before this node's stores)
             // ---- output: slot entries, or dense rows (overflowed / leaving the young set) ----
             const uint32_t total = (uint32_t)wave_sum((unsigned long long)cnt_sp);
             const bool overflow = total > a.cap;
             uint16_t* out = a.slot_next + v * kSlotU16;
+            // the slot is staged in LDS and written as whole lines (no partial-line writes)
             if (!overflow && total) {
                 uint32_t base = 1;
                 for (uint32_t t0 = 0; t0 < ntouch; t0 += 64) {
@@ -282,13 +273,19 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
                     while (x) {
                         const uint32_t bb = (uint32_t)__builtin_ctzll(x);
                         x &= x - 1ull;
-                        out[pos++] = (uint16_t)(((uint32_t)yt.w_idx << 10) | ((i & 15u) << 6) | bb);
+                        s_out[pos++] = (uint16_t)(((uint32_t)yt.w_idx << 10) | ((i & 15u) << 6) | bb);
                     }
                     base += (uint32_t)wave_sum((unsigned long long)c);
                 }
             }
-            if (lane == 0) out[0] = (uint16_t)(overflow ? kSlotOverflow : total);
-            t_slw += 1u + (total > 63u && !overflow ? 1u : 0u);
+            if (lane == 0) s_out[0] = (uint16_t)(overflow ? kSlotOverflow : total);
+            __builtin_amdgcn_wave_barrier();
+            {
+                const uint32_t lines = (!overflow && total > 63u) ? 2u : 1u;
+                if (lane < 8u * lines)
+                    *reinterpret_cast<ulonglong2*>(out + lane * 8u) = *reinterpret_cast<const ulonglong2*>(s_out + lane * 8u);
+                t_slw += lines;
+            }
             // dense rows: the leaving tiles [0, nt) always; every write-sparse tile if overflowed
             const uint32_t ndense = overflow ? a.ny : a.nt;
             unsigned long long nzw = 0ull;
