@@ -176,17 +176,22 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
                     }
 #pragma unroll
                     for (int k = 0; k < kYoungQ; k++) {
+                        if (pb + k * 8 >= np) break;  // (uniform) no peer in this group of 8
                         const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
                         const bool valid = p < 64u && (uint32_t)__shfl((int)cid, (int)(p & 63u), 64) != 0xffffffffu;
                         const uint32_t hdr = (uint32_t)__shfl((int)(q[k].x & 0xffffull), (int)(lane & ~7u), 64);
                         t_sl += wave_count(valid && (lane & 7u) == 0u) * 2u;
-                        if (valid && hdr != kSlotOverflow) {
+                        const bool ok = valid && hdr != kSlotOverflow;
+                        const uint32_t lim = ok ? hdr : 0u;
 #pragma unroll
-                            for (int j = 0; j < 8; j++) {
-                                const uint32_t pos = (lane & 7u) * 8u + (uint32_t)j;
-                                if (pos >= 1u && pos <= hdr) scatter(slot_entry(q[k], j));
-                                if (64u + pos <= hdr) scatter(slot_entry(q2[k], j));
-                            }
+                        for (int j = 0; j < 8; j++) {
+                            const uint32_t pos = (lane & 7u) * 8u + (uint32_t)j;
+                            if (pos >= 1u && pos <= lim) scatter(slot_entry(q[k], j));
+                        }
+                        if (__ballot(lim > 63u)) {  // (uniform) some peer has a second line
+#pragma unroll
+                            for (int j = 0; j < 8; j++)
+                                if (64u + (lane & 7u) * 8u + (uint32_t)j <= lim) scatter(slot_entry(q2[k], j));
                         }
                         const unsigned long long mo = __ballot((lane & 7u) == 0u && valid && hdr == kSlotOverflow);
                         if (mo) {
