@@ -38,7 +38,10 @@ def main():
     ap.add_argument("--passes", type=int, default=1,
                     help="engine passes in the run (share shards per GPU): the timed "
                          "dispatches are the last K of each pass")
-    ap.add_argument("--kernel", default="k_pull")
+    ap.add_argument("--kernel", default="k_pull<", help="substring of the kernel name")
+    ap.add_argument("--bench-json", help="the JSON line the profiled bench.py printed: its config "
+                                         "is recorded so bench.py attaches this traffic only to "
+                                         "lines of the same configuration")
     ap.add_argument("--out")
     a = ap.parse_args()
     def timed(v):  # the last K dispatches of each engine pass
@@ -60,6 +63,15 @@ def main():
         "hbm_bytes_per_launch": (2 * fetch_kib + write_kib) * 1024,
         "note": "read = 2 x FETCH_SIZE (gfx950 half-count for 16-B/lane reads), KiB -> bytes",
     }
+    if a.bench_json:
+        with open(a.bench_json) as fh:
+            line = json.loads([ln for ln in fh.read().splitlines() if ln.startswith("{")][-1])
+        out["config"] = {"workload": "C4" if "10M nodes" in line["config"]["workload"] else "C3",
+                         "warmup": line["warmup"], "steps": line["steps"],
+                         "live_words_per_node": line["config"]["live_words_per_node"],
+                         "pull_variant": line["roofline"]["pull_variant"]}
+        out["algorithmic_bytes_per_launch"] = line["roofline"]["bytes_per_launch"]
+        out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / line["roofline"]["bytes_per_launch"]
     s = json.dumps(out, indent=1)
     if a.out:
         with open(a.out, "w") as fh:

@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--passes", type=int, default=1,
                     help="engine passes in the run (share shards per GPU): the timed "
                          "dispatches are the last K of each pass")
-    ap.add_argument("--kernel", default="k_pull")
+    ap.add_argument("--kernel", default="k_pull<", help="substring of the kernel name")
     ap.add_argument("--out")
     a = ap.parse_args()
     stats = list(csv.DictReader(open(os.path.join(a.prof_dir, f"{a.run}_kernel_stats.csv"))))
