@@ -189,6 +189,19 @@ int gossip_engine_set_row_partition(gossip_engine* e, uint32_t rank, uint32_t co
 int gossip_rccl_unique_id(uint8_t* out, uint32_t len); /* len >= 128 (ncclUniqueId) */
 int gossip_engine_connect_rccl(gossip_engine* e, const uint8_t* unique_id, uint32_t len);
 int gossip_engine_group_run(gossip_engine** engines, uint32_t count, int64_t tick_end);
+/* The exchange moves only OCCUPIED 16-word tile rows of F_next (the tile-occupancy bits), with
+ * the occupancy words, per-node row offsets and the rank's liveness words: one message per rank
+ * and tick.  Host-staged backend (any transport: gloo, MPI, sockets): per tick every rank calls
+ *   gossip_engine_tick_begin       pull + births of the tick, packs the rank's message
+ *                                  (returns 1 instead of 0 when the run is complete)
+ *   gossip_engine_exchange_export  copies the message to host memory (buf NULL: size only)
+ *   gossip_engine_exchange_import  once per other rank, with that rank's message
+ *   gossip_engine_tick_end         liveness, retirement, next tick
+ * The messages are exactly those the RCCL backend broadcasts. */
+int gossip_engine_tick_begin(gossip_engine* e);
+int gossip_engine_exchange_export(gossip_engine* e, void* buf, uint64_t cap_bytes, uint64_t* bytes);
+int gossip_engine_exchange_import(gossip_engine* e, uint32_t rank, const void* buf, uint64_t bytes);
+int gossip_engine_tick_end(gossip_engine* e);
 
 /* NS-3 link timing: every hop of a share costs
  *     latency + send_defer_ns + (len(message) + header_bytes) * ns_per_byte
@@ -280,6 +293,10 @@ typedef struct gossip_counters {
     uint64_t young_seen_writes;   /* own seen words written [8 B]                        */
     uint64_t young_rows_written;  /* dense tile rows written [128 B]                     */
     uint64_t young_slot_writes;   /* slot lines written [128 B]                          */
+    /* row partition: bytes of the compressed frontier exchange (packed own rows sent,
+       other ranks' rows received) since creation                                            */
+    uint64_t exchange_bytes_sent;
+    uint64_t exchange_bytes_received;
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 int gossip_engine_reset_timing(gossip_engine* e);

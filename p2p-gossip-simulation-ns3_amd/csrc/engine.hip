@@ -23,6 +23,7 @@
 //               same-tick "own generation vs arrival" rule for id groups.
 //   k_reduce -- counter reductions for snapshots / totals.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -469,8 +470,6 @@ struct gossip_engine {
     uint32_t row_rank = 0, row_count = 1, v0 = 0, v1 = 0;
     std::vector<uint32_t> row_lo;  // rank r owns [row_lo[r], row_lo[r + 1])
     ncclComm_t comm = nullptr;
-    unsigned long long* d_live_all = nullptr;  // [row_count][live_all_cap] partial liveness
-    uint32_t live_all_cap = 0;
     uint32_t link_hdr = 0;
     std::vector<int64_t> ev_delta;
     uint64_t* d_smask[4] = {};            // per ring slot: snapshot masks [snap][word]
@@ -587,6 +586,22 @@ struct gossip_engine {
     int tick_step_a(int64_t t);  // up to the tick's kernels (pull, births, snapshot counts)
     int tick_step_b(int64_t t);  // exchange (RCCL) + liveness read-back + bookkeeping
     int exchange_rccl(int64_t t);
+    // compressed row exchange (row partition): message buffers and traffic counters
+    int pack_rows(int64_t t);
+    int unpack_rows(int64_t t, uint32_t r, const uint64_t* msg, uint64_t words);
+    int ensure_dev(uint64_t*& p, uint64_t& cap, uint64_t words);
+    uint64_t* d_msg = nullptr;       // this rank's packed message
+    uint64_t msg_cap = 0, msg_words = 0;
+    uint32_t* d_cnt = nullptr;
+    uint64_t cnt_cap = 0;
+    void* d_scan_tmp = nullptr;
+    size_t scan_tmp_bytes = 0;
+    uint64_t* d_recv_msgs = nullptr;  // the other ranks' messages (RCCL / host-staged import)
+    uint64_t recv_cap = 0;
+    uint64_t* d_sizes = nullptr;
+    uint64_t sizes_cap = 0;
+    uint64_t exchange_bytes_out = 0, exchange_bytes_in = 0;
+    bool tick_open = false;          // host-staged stepping: tick_begin done, tick_end pending
     int retire_from(int64_t known_tick, const unsigned long long* live);
     int alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t);
     int grow(uint32_t new_stride);
@@ -609,7 +624,7 @@ gossip_engine::~gossip_engine() {
     hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
-    hipFree(d_live_all);
+    hipFree(d_msg); hipFree(d_cnt); hipFree(d_scan_tmp); hipFree(d_recv_msgs); hipFree(d_sizes);
     hipFree(d_slot[0]); hipFree(d_slot[1]);
     for (int k = 0; k < kRing; k++) { hipFree(d_young[k]); hipHostFree(h_young[k]); }
     for (auto& p : timers_young) {
@@ -1476,16 +1491,81 @@ int gossip_engine::tick_step_a(int64_t t) {
     return GOSSIP_OK;
 }
 
-// Row partition over RCCL: every rank broadcasts its rows of F_next and of their tile
-// occupancy (an all-gather with per-rank block sizes) and all-gathers its partial liveness
-// words, which k_or_rows folds into the tick's global liveness.
-__global__ void k_or_rows(const unsigned long long* __restrict__ parts, uint32_t nparts, uint32_t cap,
-                          uint32_t wact, unsigned long long* __restrict__ live) {
+// ---- compressed row exchange (row partition) --------------------------------------------
+// A rank's message for tick t: its rows [lo, hi) of F_next, restricted to OCCUPIED 16-word tile
+// rows (the nz bits; unoccupied rows hold stale words no reader loads), plus its partial
+// liveness.  Layout in uint64 words:
+//   [0]                      number of rows R
+//   [1, 1 + m)               nz words of rows lo..hi-1 (m = (hi - lo) * ntw)
+//   [.., + ceil((k+1)/2))    uint32 row offsets: rows of node lo+i start at offset[i] (k = hi-lo)
+//   [.., + 16 R)             the rows, node by node, tile by tile
+//   [.., + wact)             liveness words of this rank's rows
+struct PackLayout {
+    uint64_t nz, off, rows, live, total;
+};
+PackLayout pack_layout(uint64_t k, uint32_t ntw, uint64_t nrows, uint32_t wact) {
+    PackLayout L;
+    L.nz = 1;
+    L.off = L.nz + k * ntw;
+    L.rows = L.off + (k + 2) / 2;
+    L.live = L.rows + 16 * nrows;
+    L.total = L.live + wact;
+    return L;
+}
+
+// per node: number of occupied tile rows; nz words copied into the message
+__global__ __launch_bounds__(256) void k_pack_count(const unsigned long long* __restrict__ nz, uint64_t k, uint32_t ntw,
+                                                    uint64_t* __restrict__ msg_nz, uint32_t* __restrict__ cnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i > k) return;
+    if (i == k) {
+        cnt[i] = 0u;  // the scan's last element = total
+        return;
+    }
+    uint32_t c = 0;
+    for (uint32_t w = 0; w < ntw; w++) {
+        const unsigned long long x = nz[i * ntw + w];
+        msg_nz[i * ntw + w] = x;
+        c += (uint32_t)__popcll(x);
+    }
+    cnt[i] = c;
+}
+
+// one wave per node: its occupied tile rows, 4 rows per instruction (16 lanes x 8 B each)
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_move_rows(uint64_t* __restrict__ F, uint32_t stride, uint64_t lo, uint64_t k,
+                                                   const uint64_t* __restrict__ nz, uint32_t ntw,
+                                                   const uint32_t* __restrict__ off, uint64_t* __restrict__ rows) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    for (uint64_t i = wave; i < k; i += nwaves) {
+        uint64_t o = off[i];
+        for (uint32_t w = 0; w < ntw; w++) {
+            unsigned long long m = (unsigned long long)nz[i * ntw + w];
+            while (m) {
+                // the g-th of the next 4 set bits goes to lanes 16g .. 16g+15
+                const uint32_t g = lane >> 4;
+                unsigned long long mm = m;
+                for (uint32_t r = 0; r < g && mm; r++) mm &= mm - 1ull;
+                const uint32_t cntb = (uint32_t)min(4, __popcll(m));
+                if (g < cntb) {
+                    const uint32_t tile = w * 64u + (uint32_t)__builtin_ctzll(mm);
+                    uint64_t* frow = F + (lo + i) * stride + (uint64_t)tile * 16u + (lane & 15u);
+                    uint64_t* mrow = rows + (o + g) * 16u + (lane & 15u);
+                    if (PACK) *mrow = *frow;
+                    else *frow = *mrow;
+                }
+                for (uint32_t r = 0; r < cntb; r++) m &= m - 1ull;
+                o += cntb;
+            }
+        }
+    }
+}
+
+__global__ void k_or_words(const uint64_t* __restrict__ src, uint32_t n, unsigned long long* __restrict__ dst) {
     const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= wact) return;
-    unsigned long long x = 0ull;
-    for (uint32_t r = 0; r < nparts; r++) x |= parts[(uint64_t)r * cap + w];
-    live[w] = x;
+    if (w < n && src[w]) dst[w] |= src[w];
 }
 
 #define NCCL_TRY(x)                                                                         \
@@ -1494,35 +1574,128 @@ __global__ void k_or_rows(const unsigned long long* __restrict__ parts, uint32_t
         if (r_ != ncclSuccess) return set_error(GOSSIP_EHIP, std::string("RCCL: ") + ncclGetErrorString(r_)); \
     } while (0)
 
-int gossip_engine::exchange_rccl(int64_t t) {
+int gossip_engine::ensure_dev(uint64_t*& p, uint64_t& cap, uint64_t words) {
+    if (words <= cap) return GOSSIP_OK;
+    HIP_TRY(hipStreamSynchronize(stream));
+    hipFree(p);
+    p = nullptr;
+    cap = std::max<uint64_t>(words, cap + cap / 2);
+    HIP_TRY(hipMalloc(&p, cap * 8));
+    return GOSSIP_OK;
+}
+
+// Pack this rank's rows of F_next (after this tick's pull and births) into d_msg; msg_words = size.
+int gossip_engine::pack_rows(int64_t t) {
     const int nxt = fcur ^ 1, lv = (int)(t % 3);
+    const uint64_t k = v1 - v0;
     const uint32_t wact = hw;
-    if (wact > live_all_cap) {
+    int rc = ensure_dev(d_msg, msg_cap, pack_layout(k, ntw, 0, wact).rows);
+    if (rc) return rc;
+    if (k + 1 > cnt_cap) {
         HIP_TRY(hipStreamSynchronize(stream));
-        hipFree(d_live_all);
-        d_live_all = nullptr;
-        live_all_cap = std::max(wact, stride);
-        HIP_TRY(hipMalloc(&d_live_all, (size_t)row_count * live_all_cap * 8));
+        hipFree(d_cnt);
+        cnt_cap = k + 1;
+        HIP_TRY(hipMalloc(&d_cnt, cnt_cap * 4));
     }
-    NCCL_TRY(ncclGroupStart());
-    for (uint32_t r = 0; r < row_count; r++) {
-        const uint64_t lo = row_lo[r], hi = row_lo[r + 1];
-        if (hi <= lo) continue;
-        NCCL_TRY(ncclBroadcast(d_F[nxt] + lo * stride, d_F[nxt] + lo * stride, (hi - lo) * stride, ncclUint64,
-                               (int)r, comm, stream));
-        if (d_nz[nxt])
-            NCCL_TRY(ncclBroadcast(d_nz[nxt] + lo * ntw, d_nz[nxt] + lo * ntw, (hi - lo) * ntw, ncclUint64,
-                                   (int)r, comm, stream));
+    const PackLayout L0 = pack_layout(k, ntw, 0, wact);
+    uint32_t* off = reinterpret_cast<uint32_t*>(d_msg + L0.off);
+    k_pack_count<<<(uint32_t)((k + 1 + 255) / 256), 256, 0, stream>>>(d_nz[nxt] + (uint64_t)v0 * ntw, k, ntw,
+                                                                      d_msg + L0.nz, d_cnt);
+    HIP_TRY(hipGetLastError());
+    size_t tmp = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d_cnt, off, (int)(k + 1), stream));
+    if (tmp > scan_tmp_bytes) {
+        HIP_TRY(hipStreamSynchronize(stream));
+        hipFree(d_scan_tmp);
+        scan_tmp_bytes = tmp;
+        HIP_TRY(hipMalloc(&d_scan_tmp, tmp));
     }
-    if (wact)
-        for (uint32_t r = 0; r < row_count; r++)  // all-gather into a [rank][cap] layout
-            NCCL_TRY(ncclBroadcast(d_live[lv], d_live_all + (uint64_t)r * live_all_cap, wact, ncclUint64,
-                                   (int)r, comm, stream));
-    NCCL_TRY(ncclGroupEnd());
-    if (wact) {
-        k_or_rows<<<(wact + 255) / 256, 256, 0, stream>>>(d_live_all, row_count, live_all_cap, wact, d_live[lv]);
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(d_scan_tmp, tmp, d_cnt, off, (int)(k + 1), stream));
+    uint32_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, off + k, 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    const PackLayout L = pack_layout(k, ntw, total, wact);
+    // (the layout's header parts do not depend on the row count: grow keeping them)
+    if (L.total > msg_cap) {
+        uint64_t* nm = nullptr;
+        HIP_TRY(hipMalloc(&nm, L.total * 8));
+        HIP_TRY(hipMemcpyAsync(nm, d_msg, L.rows * 8, hipMemcpyDeviceToDevice, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        hipFree(d_msg);
+        d_msg = nm;
+        msg_cap = L.total;
+        off = reinterpret_cast<uint32_t*>(d_msg + L.off);
+    }
+    const unsigned long long hdr = total;
+    HIP_TRY(hipMemcpyAsync(d_msg, &hdr, 8, hipMemcpyHostToDevice, stream));
+    if (total) {
+        const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((k + 3) / 4, 4096));
+        k_move_rows<true><<<g, 256, 0, stream>>>(d_F[nxt], stride, v0, k, d_msg + L.nz, ntw, off, d_msg + L.rows);
         HIP_TRY(hipGetLastError());
     }
+    if (wact) HIP_TRY(hipMemcpyAsync(d_msg + L.live, d_live[lv], (size_t)wact * 8, hipMemcpyDeviceToDevice, stream));
+    msg_words = L.total;
+    exchange_bytes_out += L.total * 8;
+    return GOSSIP_OK;
+}
+
+// Unpack rank r's message (device buffer) into this engine's F_next, nz_next and liveness.
+int gossip_engine::unpack_rows(int64_t t, uint32_t r, const uint64_t* msg, uint64_t words) {
+    const int nxt = fcur ^ 1, lv = (int)(t % 3);
+    const uint64_t lo = row_lo[r], k = row_lo[r + 1] - row_lo[r];
+    const uint32_t wact = hw;
+    unsigned long long total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, msg, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    const PackLayout L = pack_layout(k, ntw, total, wact);
+    if (L.total != words) return set_error(GOSSIP_EINVAL, "row exchange: message of rank " + std::to_string(r) +
+                                                          " has the wrong size (ranks diverged?)");
+    HIP_TRY(hipMemcpyAsync(d_nz[nxt] + lo * ntw, msg + L.nz, (size_t)k * ntw * 8, hipMemcpyDeviceToDevice, stream));
+    if (total) {
+        const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((k + 3) / 4, 4096));
+        k_move_rows<false><<<g, 256, 0, stream>>>(d_F[nxt], stride, lo, k, msg + L.nz, ntw,
+                                                  reinterpret_cast<const uint32_t*>(msg + L.off),
+                                                  const_cast<uint64_t*>(msg + L.rows));
+        HIP_TRY(hipGetLastError());
+    }
+    if (wact) {
+        k_or_words<<<(wact + 255) / 256, 256, 0, stream>>>(msg + L.live, wact, d_live[lv]);
+        HIP_TRY(hipGetLastError());
+    }
+    exchange_bytes_in += words * 8;
+    return GOSSIP_OK;
+}
+
+// Row partition over RCCL: every rank packs its occupied rows, the message sizes are
+// all-gathered, then each rank's message is broadcast (an all-gather with per-rank sizes) and
+// unpacked by the others -- on the engine's stream.
+int gossip_engine::exchange_rccl(int64_t t) {
+    int rc = pack_rows(t);
+    if (rc) return rc;
+    int rc2 = ensure_dev(d_sizes, sizes_cap, row_count);
+    if (rc2) return rc2;
+    const unsigned long long mine = msg_words;
+    HIP_TRY(hipMemcpyAsync(d_sizes + row_rank, &mine, 8, hipMemcpyHostToDevice, stream));
+    NCCL_TRY(ncclAllGather(d_sizes + row_rank, d_sizes, 1, ncclUint64, comm, stream));
+    std::vector<unsigned long long> sz(row_count);
+    HIP_TRY(hipMemcpyAsync(sz.data(), d_sizes, row_count * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    uint64_t tot = 0;
+    std::vector<uint64_t> at(row_count);
+    for (uint32_t r = 0; r < row_count; r++) {
+        at[r] = tot;
+        tot += r == row_rank ? 0 : sz[r];
+    }
+    rc = ensure_dev(d_recv_msgs, recv_cap, std::max<uint64_t>(tot, 1));
+    if (rc) return rc;
+    NCCL_TRY(ncclGroupStart());
+    for (uint32_t r = 0; r < row_count; r++) {
+        uint64_t* buf = r == row_rank ? d_msg : d_recv_msgs + at[r];
+        NCCL_TRY(ncclBroadcast(buf, buf, sz[r], ncclUint64, (int)r, comm, stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    for (uint32_t r = 0; r < row_count; r++)
+        if (r != row_rank && (rc = unpack_rows(t, r, d_recv_msgs + at[r], sz[r]))) return rc;
     return GOSSIP_OK;
 }
 
@@ -1837,7 +2010,6 @@ int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end
     gossip_engine* e0 = es[0];
     if (tick_end > e0->tick_end) tick_end = e0->tick_end;
     try {
-        std::vector<unsigned long long> acc, part;
         while (e0->cur < tick_end) {
             if (e0->batch && e0->cur > e0->last_birth_tick &&
                 std::find(e0->tile_alloc.begin(), e0->tile_alloc.end(), (uint8_t)1) == e0->tile_alloc.end()) {
@@ -1853,30 +2025,24 @@ int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end
                 if (rc) return rc;
                 HIP_TRY(hipStreamSynchronize(es[r]->stream));
             }
-            const int nxt = e0->fcur ^ 1, lv = (int)(t % 3);
-            const uint32_t wact = e0->hw, stride = e0->stride, ntw = e0->ntw;
             for (uint32_t r = 1; r < count; r++)
-                if (es[r]->hw != wact || es[r]->stride != stride || es[r]->fcur != e0->fcur)
+                if (es[r]->hw != e0->hw || es[r]->stride != e0->stride || es[r]->fcur != e0->fcur)
                     return set_error(GOSSIP_EINVAL, "row partition engines diverged (different inputs?)");
-            for (uint32_t d = 0; d < count; d++)
+            // the compressed exchange of the RCCL backend, with device-to-device reads
+            for (uint32_t r = 0; r < count; r++) {
+                HIP_TRY(hipSetDevice(es[r]->device));
+                int rc = es[r]->pack_rows(t);
+                if (rc) return rc;
+                HIP_TRY(hipStreamSynchronize(es[r]->stream));
+            }
+            for (uint32_t d = 0; d < count; d++) {
+                HIP_TRY(hipSetDevice(es[d]->device));
                 for (uint32_t r = 0; r < count; r++) {
-                    const uint64_t lo = e0->row_lo[r], hi = e0->row_lo[r + 1];
-                    if (r == d || hi <= lo) continue;
-                    HIP_TRY(hipMemcpy(es[d]->d_F[nxt] + lo * stride, es[r]->d_F[nxt] + lo * stride,
-                                      (hi - lo) * stride * 8, hipMemcpyDeviceToDevice));
-                    if (es[d]->d_nz[nxt])
-                        HIP_TRY(hipMemcpy(es[d]->d_nz[nxt] + lo * ntw, es[r]->d_nz[nxt] + lo * ntw,
-                                          (hi - lo) * ntw * 8, hipMemcpyDeviceToDevice));
+                    if (r == d) continue;
+                    int rc = es[d]->unpack_rows(t, r, es[r]->d_msg, es[r]->msg_words);
+                    if (rc) return rc;
                 }
-            if (wact) {
-                acc.assign(wact, 0ull);
-                part.resize(wact);
-                for (uint32_t r = 0; r < count; r++) {
-                    HIP_TRY(hipMemcpy(part.data(), es[r]->d_live[lv], (size_t)wact * 8, hipMemcpyDeviceToHost));
-                    for (uint32_t w = 0; w < wact; w++) acc[w] |= part[w];
-                }
-                for (uint32_t r = 0; r < count; r++)
-                    HIP_TRY(hipMemcpy(es[r]->d_live[lv], acc.data(), (size_t)wact * 8, hipMemcpyHostToDevice));
+                HIP_TRY(hipStreamSynchronize(es[d]->stream));
             }
             for (uint32_t r = 0; r < count; r++) {
                 HIP_TRY(hipSetDevice(es[r]->device));
@@ -1924,6 +2090,78 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     } else {
         return set_error(GOSSIP_EINVAL, "unknown option '" + k + "'");
     }
+    return GOSSIP_OK;
+}
+
+// Host-staged exchange (any transport): tick_begin -> export own message -> import every other
+// rank's -> tick_end.
+static int check_stepping(gossip_engine* e) {
+    if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    if (!e->have_sched) return set_error(GOSSIP_ESTATE, "set graph and schedule first");
+    if (e->comm) return set_error(GOSSIP_ESTATE, "host-staged stepping is not for an RCCL-connected engine");
+    return GOSSIP_OK;
+}
+
+int gossip_engine_tick_begin(gossip_engine* e) {
+    int rc = check_stepping(e);
+    if (rc) return rc;
+    if (e->tick_open) return set_error(GOSSIP_ESTATE, "tick_begin twice without tick_end");
+    HIP_TRY(hipSetDevice(e->device));
+    try {
+        if (e->cur >= e->tick_end) return 1;
+        if (e->batch && e->cur > e->last_birth_tick &&
+            std::find(e->tile_alloc.begin(), e->tile_alloc.end(), (uint8_t)1) == e->tile_alloc.end()) {
+            e->done = true;
+            return 1;
+        }
+        if ((rc = e->tick_step_a(e->cur))) return rc;
+        if ((rc = e->pack_rows(e->cur))) return rc;
+        HIP_TRY(hipStreamSynchronize(e->stream));
+    } catch (const std::bad_alloc&) {
+        return set_error(GOSSIP_ENOMEM, "host allocation failed");
+    }
+    e->tick_open = true;
+    return GOSSIP_OK;
+}
+
+int gossip_engine_exchange_export(gossip_engine* e, void* buf, uint64_t cap_bytes, uint64_t* bytes) {
+    int rc = check_stepping(e);
+    if (rc) return rc;
+    if (!e->tick_open) return set_error(GOSSIP_ESTATE, "exchange_export outside tick_begin/tick_end");
+    if (bytes) *bytes = e->msg_words * 8;
+    if (!buf) return GOSSIP_OK;
+    if (cap_bytes < e->msg_words * 8) return set_error(GOSSIP_EINVAL, "export buffer too small");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipMemcpy(buf, e->d_msg, e->msg_words * 8, hipMemcpyDeviceToHost));
+    return GOSSIP_OK;
+}
+
+int gossip_engine_exchange_import(gossip_engine* e, uint32_t rank, const void* buf, uint64_t bytes) {
+    int rc = check_stepping(e);
+    if (rc) return rc;
+    if (!e->tick_open) return set_error(GOSSIP_ESTATE, "exchange_import outside tick_begin/tick_end");
+    if (rank >= e->row_count || rank == e->row_rank || !buf || bytes % 8)
+        return set_error(GOSSIP_EINVAL, "exchange_import: bad rank or buffer");
+    HIP_TRY(hipSetDevice(e->device));
+    if ((rc = e->ensure_dev(e->d_recv_msgs, e->recv_cap, std::max<uint64_t>(bytes / 8, 1)))) return rc;
+    HIP_TRY(hipMemcpyAsync(e->d_recv_msgs, buf, bytes, hipMemcpyHostToDevice, e->stream));
+    if ((rc = e->unpack_rows(e->cur, rank, e->d_recv_msgs, bytes / 8))) return rc;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return GOSSIP_OK;
+}
+
+int gossip_engine_tick_end(gossip_engine* e) {
+    int rc = check_stepping(e);
+    if (rc) return rc;
+    if (!e->tick_open) return set_error(GOSSIP_ESTATE, "tick_end without tick_begin");
+    HIP_TRY(hipSetDevice(e->device));
+    try {
+        if ((rc = e->tick_step_b(e->cur))) return rc;
+    } catch (const std::bad_alloc&) {
+        return set_error(GOSSIP_ENOMEM, "host allocation failed");
+    }
+    e->cur++;
+    e->tick_open = false;
     return GOSSIP_OK;
 }
 
@@ -2069,7 +2307,8 @@ int gossip_engine_run(gossip_engine* e, int64_t tick_end) {
     if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
     if (!e->have_sched) return set_error(GOSSIP_ESTATE, "set graph and schedule first");
     if (e->row_count > 1 && !e->comm)
-        return set_error(GOSSIP_ESTATE, "row-partitioned engine: gossip_engine_connect_rccl or gossip_engine_group_run");
+        return set_error(GOSSIP_ESTATE, "row-partitioned engine: gossip_engine_connect_rccl or gossip_engine_group_run "
+                                        "(or host-staged gossip_engine_tick_begin/exchange/tick_end)");
     HIP_TRY(hipSetDevice(e->device));
     if (tick_end > e->tick_end) tick_end = e->tick_end;
     try {
@@ -2217,6 +2456,8 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
         c->young_ms = yms;
     }
     c->young_launches = e->young_launches;
+    c->exchange_bytes_sent = e->exchange_bytes_out;
+    c->exchange_bytes_received = e->exchange_bytes_in;
     c->young_slot_lines = acct[8];
     c->young_col_ids = acct[9];
     c->young_fallback_rows = acct[10];

@@ -55,7 +55,8 @@ EXPORTED_SYMBOLS = (
     "gossip_format_statistics", "gossip_format_periodic", "gossip_engine_set_link_timing",
     "gossip_share_message_length", "gossip_format_event_log", "gossip_engine_set_row_partition",
     "gossip_rccl_unique_id", "gossip_engine_connect_rccl", "gossip_engine_group_run",
-    "gossip_engine_set_option", "gossip_engine_mode",
+    "gossip_engine_set_option", "gossip_engine_mode", "gossip_engine_tick_begin",
+    "gossip_engine_exchange_export", "gossip_engine_exchange_import", "gossip_engine_tick_end",
 )
 
 # NS-3 5 Mbps point-to-point links (p2pnetwork.cc:113): ns per byte, PPP+IPv4+TCP(timestamp
@@ -101,6 +102,7 @@ class gossip_counters(C.Structure):
         ("young_col_ids", C.c_uint64), ("young_fallback_rows", C.c_uint64),
         ("young_seen_reads", C.c_uint64), ("young_seen_writes", C.c_uint64),
         ("young_rows_written", C.c_uint64), ("young_slot_writes", C.c_uint64),
+        ("exchange_bytes_sent", C.c_uint64), ("exchange_bytes_received", C.c_uint64),
     ]
 
 
@@ -154,6 +156,10 @@ def load_library(path: str = LIB_PATH):
         "gossip_engine_group_run": (C.c_int, [P, u32, i64]),
         "gossip_engine_set_option": (C.c_int, [P, C.c_char_p, i64]),
         "gossip_engine_mode": (C.c_int, [P]),
+        "gossip_engine_tick_begin": (C.c_int, [P]),
+        "gossip_engine_exchange_export": (C.c_int, [P, P, u64, C.POINTER(u64)]),
+        "gossip_engine_exchange_import": (C.c_int, [P, u32, P, u64]),
+        "gossip_engine_tick_end": (C.c_int, [P]),
         "gossip_format_event_log": (i64, [P, u64, P, u64, P, P, P, P, i64, i64, i64, i64, u32,
                                           i64, C.c_int, C.c_char_p, u64]),
         "gossip_engine_first_tick": (i64, [P]),
@@ -359,6 +365,31 @@ class Engine:
     def connect_rccl(self, unique_id: bytes):
         _check(load_library().gossip_engine_connect_rccl(self._h, unique_id, len(unique_id)),
                "rccl connect")
+
+    # ---- host-staged row exchange (gossip.h): one message per rank and tick ----
+    def tick_begin(self) -> bool:
+        """Pull + births of the next tick and pack this rank's rows; False when the run is done."""
+        rc = load_library().gossip_engine_tick_begin(self._h)
+        if rc == 1:
+            return False
+        _check(rc, "tick begin")
+        return True
+
+    def exchange_export(self) -> np.ndarray:
+        lib = load_library()
+        n = C.c_uint64()
+        _check(lib.gossip_engine_exchange_export(self._h, None, 0, C.byref(n)), "export size")
+        buf = np.empty(n.value // 8, np.uint64)
+        _check(lib.gossip_engine_exchange_export(self._h, _vp(buf), buf.nbytes, C.byref(n)), "export")
+        return buf
+
+    def exchange_import(self, rank: int, msg: np.ndarray):
+        msg = np.ascontiguousarray(msg, np.uint64)
+        _check(load_library().gossip_engine_exchange_import(self._h, int(rank), _vp(msg), msg.nbytes),
+               "import")
+
+    def tick_end(self):
+        _check(load_library().gossip_engine_tick_end(self._h), "tick end")
 
     def set_link_timing(self, ns_per_byte: int, header_bytes: int, send_defer_ns: int):
         _check(load_library().gossip_engine_set_link_timing(
