@@ -101,6 +101,14 @@ int gossip_schedule_create(uint32_t num_nodes, uint32_t node_seed, int64_t t_sta
                            int num_threads, gossip_schedule** out);
 int gossip_schedule_from_events(uint64_t num_events, const gossip_gen_event* ev,
                                 gossip_schedule** out);
+/* Synthetic schedule generated on GPU `device` (schedule_gpu.hip): the reference's rules --
+ * first event at U(2,5) s, then every U(2,5) s; counted iff t_start <= t < t_cut (and
+ * < t_gen_end if nonzero); shareId from GenerateUniqueShareId's formula -- with each node's
+ * U(2,5) draws taken from a counter-based Philox4x32-10 stream keyed by (seed, node) instead of
+ * the reference's mt19937(seed + node).  For large synthetic runs; not the reference's stream. */
+int gossip_schedule_create_philox(uint32_t num_nodes, uint32_t seed, int64_t t_start_ns,
+                                  int64_t t_cut_ns, int64_t t_gen_end_ns, int32_t device,
+                                  gossip_schedule** out);
 uint64_t gossip_schedule_size(const gossip_schedule* s);
 /* Events sorted by (ns, node). */
 int gossip_schedule_get(const gossip_schedule* s, gossip_gen_event* out);

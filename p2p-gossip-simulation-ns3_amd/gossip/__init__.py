@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "gossip_rccl_unique_id", "gossip_engine_connect_rccl", "gossip_engine_group_run",
     "gossip_engine_set_option", "gossip_engine_mode", "gossip_engine_tick_begin",
     "gossip_engine_exchange_export", "gossip_engine_exchange_import", "gossip_engine_tick_end",
+    "gossip_schedule_create_philox",
 )
 
 # NS-3 5 Mbps point-to-point links (p2pnetwork.cc:113): ns per byte, PPP+IPv4+TCP(timestamp
@@ -138,6 +139,7 @@ def load_library(path: str = LIB_PATH):
         "gossip_topology_destroy": (None, [P]),
         "gossip_schedule_create": (C.c_int, [u32, u32, i64, i64, i64, u32, C.c_int, C.POINTER(P)]),
         "gossip_schedule_from_events": (C.c_int, [u64, P, C.POINTER(P)]),
+        "gossip_schedule_create_philox": (C.c_int, [u32, u32, i64, i64, i64, i32, C.POINTER(P)]),
         "gossip_schedule_size": (u64, [P]),
         "gossip_schedule_get": (C.c_int, [P, P]),
         "gossip_schedule_destroy": (None, [P]),
@@ -286,6 +288,24 @@ def make_schedule(n: int, node_seed: int, t_start_ns: int, t_cut_ns: int, t_gen_
     h = C.c_void_p()
     _check(lib.gossip_schedule_create(n, node_seed, t_start_ns, t_cut_ns, t_gen_end_ns, id_mask,
                                       threads, C.byref(h)), "schedule")
+    try:
+        m = int(lib.gossip_schedule_size(h))
+        ev = np.empty(m, GEN_EVENT_DTYPE)
+        if m:
+            _check(lib.gossip_schedule_get(h, _vp(ev)), "schedule get")
+        return ev
+    finally:
+        lib.gossip_schedule_destroy(h)
+
+
+def make_schedule_philox(n: int, seed: int, t_start_ns: int, t_cut_ns: int, t_gen_end_ns: int = 0,
+                         device: int = 0) -> np.ndarray:
+    """Synthetic schedule generated on the GPU from per-node Philox4x32-10 streams (gossip.h
+    gossip_schedule_create_philox): the reference's rules, not its mt19937 stream."""
+    lib = load_library()
+    h = C.c_void_p()
+    _check(lib.gossip_schedule_create_philox(n, seed, t_start_ns, t_cut_ns, t_gen_end_ns, device,
+                                             C.byref(h)), "philox schedule")
     try:
         m = int(lib.gossip_schedule_size(h))
         ev = np.empty(m, GEN_EVENT_DTYPE)
