@@ -46,8 +46,10 @@ def test_gpu_schedule_window_and_rate(gossip):
     assert np.all(np.diff(ev["ns"]) >= 0)
     same = np.diff(ev["ns"]) == 0
     assert np.all(np.diff(ev["node"].astype(np.int64))[same] > 0)  # (ns, node) order
-    # renewal process with mean interval 3.5 s, started at t = 0: ~2 s x n / 3.5 s events
-    assert abs(len(ev) / (2.0 * n / 3.5) - 1.0) < 0.1
+    # the same renewal process as the reference's mt19937 schedule (started at t = 0, not yet
+    # stationary at 5-7 s): the two event counts agree to sampling noise (~0.15 %)
+    ref = gossip.make_schedule(n, 5, T0, gossip.seconds_to_ns(59.9), t_gen_end_ns=t_end, threads=16)
+    assert abs(len(ev) / len(ref) - 1.0) < 0.01
     # a node's events are >= 2 s apart: at most one per node in a 2 s window
     assert len(np.unique(ev["node"])) == len(ev)
 
