@@ -53,6 +53,7 @@ struct Options {
     uint32_t shards = 0;               // share shards (0: gpus); doubled on capacity errors
     std::string layout = "shards";     // shards | rows
     double memLimitMB = 0;             // device memory budget per engine (0: the device's)
+    std::string schedule = "exact";    // exact (the reference's mt19937 stream) | philox (GPU)
 };
 
 void usage() {
@@ -65,7 +66,7 @@ void usage() {
                  "                  [--mode=auto|csr|dense] [--dumpLinks=F] [--dumpEvents=F]\n"
                  "                  [--links=F] [--events=F] [--dumpTrace=F] [--netanim=F]\n"
                  "                  [--log=F|-] [--gpus=N] [--shards=S] [--layout=shards|rows]\n"
-                 "                  [--memLimitMB=M]\n");
+                 "                  [--memLimitMB=M] [--schedule=exact|philox]\n");
 }
 
 bool parse(int argc, char** argv, Options& o) {
@@ -132,6 +133,7 @@ bool parse(int argc, char** argv, Options& o) {
         else if (key == "shards") { if (!num(d) || d < 0 || d > 4096) return false; o.shards = (uint32_t)d; }
         else if (key == "layout") { if (!need()) return false; o.layout = val; }
         else if (key == "memLimitMB") { if (!num(o.memLimitMB) || o.memLimitMB < 0) return false; }
+        else if (key == "schedule") { if (!need()) return false; o.schedule = val; }
         else {
             std::fprintf(stderr, "unknown option --%s\n", key.c_str());
             return false;
@@ -292,6 +294,12 @@ int main(int argc, char** argv) {
         while (std::fscanf(f, "%lld %u %u", &ns, &node, &id) == 3) ev.push_back({ns, node, id});
         std::fclose(f);
         if (gossip_schedule_from_events(ev.size(), ev.data(), &sched)) return die("schedule import");
+    } else if (o.schedule == "philox") {  // synthetic: per-node Philox streams, generated on the GPU
+        if (gossip_schedule_create_philox(n, o.nodeSeed, t_start, t_cut, 0, o.device, &sched))
+            return die("philox schedule");
+    } else if (o.schedule != "exact") {
+        usage();
+        return 2;
     } else if (gossip_schedule_create(n, o.nodeSeed, t_start, t_cut, 0, 0, o.threads, &sched)) {
         return die("schedule");
     }

@@ -55,6 +55,33 @@ def test_gpu_schedule_window_and_rate(gossip):
 
 
 @pytest.mark.gpu
+def test_cli_philox_schedule(gossip, oracle, tmp_path):
+    # gossip_sim --schedule=philox: the dumped schedule is the library's, the report the oracle's
+    import os
+    import subprocess
+
+    from conftest import PKG
+
+    evf = tmp_path / "ev.txt"
+    sim = os.path.join(PKG, "lib", "gossip_sim")
+    p = subprocess.run([sim, "--numNodes=300", "--connectionProb=0.03", "--simTime=14", "--seed=4",
+                        "--nodeSeed=9", "--schedule=philox", f"--dumpEvents={evf}"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    got = np.loadtxt(evf, dtype=np.int64).reshape(-1, 3)
+    t_cut = gossip.seconds_to_ns(13.9)
+    ev = gossip.make_schedule_philox(300, 9, T0, t_cut)
+    assert np.array_equal(got[:, 0], ev["ns"]) and np.array_equal(got[:, 1], ev["node"])
+    assert np.array_equal(got[:, 2], ev["share_id"])
+    topo = gossip.Topology.gnp(300, 0.03, 4, gossip.TOPO_EXACT)
+    a, b = topo.links()
+    r = oracle.run_replay(300, 5_000_000, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
+    want = gossip.format_statistics(gossip.Stats(r.gen, r.recv, r.fwd, r.sent, r.processed, r.peers,
+                                                 r.sockets))
+    assert want in p.stdout
+
+
+@pytest.mark.gpu
 def test_engine_runs_a_philox_schedule_like_the_oracle(gossip, oracle):
     n = 500
     topo = gossip.Topology.gnp(n, 0.02, 12, gossip.TOPO_EXACT)
