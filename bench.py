@@ -43,6 +43,8 @@ import gossip.workloads as WL  # noqa: E402
 # BASELINE.json "metric", quoted on C4 (10M nodes)
 BASELINE_METRIC = "share-deliveries/sec (edge events) at 10M nodes, 1/2/4/8 GPUs; % HBM/MFMA peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# the engine's young_overlap option (include/gossip.h), default 1; GOSSIP_YOUNG_OVERLAP sets it
+YOUNG_OVERLAP = int(os.environ.get("GOSSIP_YOUNG_OVERLAP", "1"))
 T0_NS = 5_000_000_000
 SLICE_NS = 10_000_000_000  # steady-state slice start (tick 2000 at 5 ms)
 L_NS = 5_000_000
@@ -113,7 +115,7 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
     acc = dict(elapsed=0.0, edges=0, gens=0, launches=0, pull_ms=0.0, moved=0, dense=0, pe=0,
                col=0, nz=0, srd=0, swr=0, fwr=0, words_hw=0, words_cap=0, dev_bytes=0, nt=0,
                grid=0, ramp_ticks=0, young_ms=0.0, young_launches=0, young_bytes=0, young_sl=0,
-               young_fb=0)
+               young_fb=0, phase_ms=0.0)
     for s in my_shards:
         t_eng = time.perf_counter()
         eng = gossip.Engine(wl["nodes"], L_NS, T0_NS, T_CUT_NS, device=local, flags=flags,
@@ -153,6 +155,10 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
         acc["young_bytes"] += c1.young_bytes_moved
         acc["young_sl"] += c1.young_slot_lines
         acc["young_fb"] += c1.young_fallback_rows
+        for k in ("young_col_ids", "young_seen_reads", "young_seen_writes", "young_rows_written",
+                  "young_slot_writes"):
+            acc[k] = acc.get(k, 0) + getattr(c1, k)
+        acc["phase_ms"] += c1.pull_phase_ms
         acc["words_hw"] = max(acc["words_hw"], c1.words_hw)
         acc["words_cap"] = max(acc["words_cap"], c1.words_cap)
         acc["dev_bytes"] = max(acc["dev_bytes"], c1.device_bytes)
@@ -322,7 +328,8 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
                 "kernel": "k_pull",
-                "pull_variant": {"nt_rows": acc["nt"], "grid": acc["grid"]},
+                "pull_variant": {"nt_rows": acc["nt"], "grid": acc["grid"],
+                                 "young_overlap": YOUNG_OVERLAP if acc["young_launches"] else None},
                 "bytes_per_launch": bytes_per_launch,
                 "bytes_note": "algorithmic bytes of the occupancy-skipping pull: the peer-row, "
                               "peer-id, occupancy, own-row and counter bytes it must move",
@@ -345,7 +352,8 @@ def main():
                         acc["moved"] - 16 * acc["pe"] - 4 * acc["col"] - 8 * acc["nz"] -
                         16 * (acc["srd"] + acc["swr"] + acc["fwr"])),
                 },
-                "pull_fraction_of_step": ((pull_ms_max + acc["young_ms"]) / (elapsed * 1e3)) if elapsed > 0 else None,
+                "pull_fraction_of_step": (((acc["phase_ms"] or (pull_ms_max + acc["young_ms"])) / (elapsed * 1e3))
+                                          if elapsed > 0 else None),
             },
         }
         if acc["young_launches"]:
@@ -359,11 +367,24 @@ def main():
                 "achieved": acc["young_bytes"] / yl / (y_ms * 1e6) if y_ms > 0 else None,
                 "slot_lines_per_launch": acc["young_sl"] / yl,
                 "fallback_rows_per_launch": acc["young_fb"] / yl,
+                "bytes_breakdown_per_launch": {
+                    "slot_lines_read": 128 * acc["young_sl"] / yl,
+                    "fallback_rows_read": 128 * acc["young_fb"] / yl,
+                    "peer_ids": 4 * acc["young_col_ids"] / yl,
+                    "own_seen_read": 8 * acc["young_seen_reads"] / yl,
+                    "own_seen_write": 8 * acc["young_seen_writes"] / yl,
+                    "dense_rows_written": 128 * acc["young_rows_written"] / yl,
+                    "slot_lines_written": 128 * acc["young_slot_writes"] / yl,
+                },
             }
-            tot_ms = avg_ms + acc["young_ms"] / max(launches, 1)
+            # wall time of the phase (HIP events around both kernels on the engine stream; they
+            # run concurrently on two streams when young_overlap is on)
+            tot_ms = (acc["phase_ms"] / max(launches, 1)) if acc["phase_ms"] else \
+                avg_ms + acc["young_ms"] / max(launches, 1)
             tot_b = bytes_per_launch + acc["young_bytes"] / max(launches, 1)
             out["roofline"]["pull_phase"] = {
-                "kernels": "k_pull + k_pull_young", "ms_per_tick": tot_ms, "bytes_per_tick": tot_b,
+                "kernels": "k_pull + k_pull_young" + (" (concurrent, two streams)" if YOUNG_OVERLAP else ""),
+                "ms_per_tick": tot_ms, "bytes_per_tick": tot_b,
                 "achieved": tot_b / (tot_ms * 1e6) if tot_ms > 0 else None,
                 "frac": (tot_b / (tot_ms * 1e6)) / HBM_PEAK_GBS if tot_ms > 0 else None}
         traffic, why = pmc_traffic(wl["name"], out)

@@ -241,6 +241,9 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *                                                                          [GOSSIP_YOUNG_AGE]
  *   "young_cap"        slot entries per node before it falls back to dense rows (1..127)
  *                                                                          [GOSSIP_YOUNG_CAP]
+ *   "young_overlap"    0: k_pull_young after k_pull on the engine stream; 1: the two run
+ *                      concurrently on two streams, k_pull_young launched first (default);
+ *                      2: concurrently, k_pull launched first            [GOSSIP_YOUNG_OVERLAP]
  *   "mem_limit"        bytes of device memory the engine may hold, 0 = what the device has
  *                      free; a window that outgrows it fails with GOSSIP_ECAPACITY / ENOMEM
  *                      (callers then split the shares into more shards)   [GOSSIP_MEM_LIMIT] */
@@ -305,6 +308,9 @@ typedef struct gossip_counters {
        other ranks' rows received) since creation                                            */
     uint64_t exchange_bytes_sent;
     uint64_t exchange_bytes_received;
+    /* wall time of the pull phase (k_pull and k_pull_young, concurrent on two streams when the
+     * young_overlap option is on), HIP events on the engine stream (TIMING) */
+    double pull_phase_ms;
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 int gossip_engine_reset_timing(gossip_engine* e);

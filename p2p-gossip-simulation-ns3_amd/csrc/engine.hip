@@ -103,6 +103,9 @@ struct PullArgs {
     unsigned long long* nz_next;
     uint32_t ntw;
     uint32_t v0 = 0;  // first node of this engine's row range (row partition; multiple of 64)
+    // 1: another kernel (k_pull_young) runs concurrently and shares the per-node outputs, so
+    // counters are added and occupancy bits OR'ed atomically (nz_next zeroed beforehand)
+    uint32_t shared_out = 0;
 };
 
 // Phase-ordered update of id groups inside one word (rare: only words holding groups).
@@ -550,6 +553,11 @@ struct gossip_engine {
     int64_t opt_young = -1;           // young tiles (k_pull_young): -1 auto, 0 off, 1 on
     int64_t opt_young_age = 5;        // write-sparse while the oldest shares are <= this many hops
     int64_t opt_young_cap = 127;      // slot entries per node before it overflows to dense rows
+    int64_t opt_young_overlap = 1;    // k_pull_young beside k_pull on a second stream (1, 2) or after (0)
+    hipStream_t ystream = nullptr;    // the second stream (created on first use)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timers_phase;  // pull phase (both kernels)
+    double phase_ms_done = 0.0;
     int64_t opt_mem_limit = 0;        // bytes of device memory the engine may hold (0: the device's)
     uint32_t last_nt = 0, last_grid = 0;  // variant of the last pull launch (counters)
     // ---- young tiles (young_kernel.h)
@@ -640,6 +648,13 @@ gossip_engine::~gossip_engine() {
         if (slot_done[k]) hipEventDestroy(slot_done[k]);
         if (live_done[k]) hipEventDestroy(live_done[k]);
     }
+    for (auto& p : timers_phase) {
+        hipEventDestroy(p.first);
+        hipEventDestroy(p.second);
+    }
+    if (ev_fork) hipEventDestroy(ev_fork);
+    if (ev_join) hipEventDestroy(ev_join);
+    if (ystream) hipStreamDestroy(ystream);
     if (stream) hipStreamDestroy(stream);
 }
 
@@ -1383,7 +1398,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                     launch_pull(lpw, epn, nt_rows, grid, pull_lds_bytes(c.wact), stream, c);
             }
         };
-        hipEvent_t e0 = nullptr, e1 = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr, p0 = nullptr, p1 = nullptr;
         a.inc = nullptr;
         if (dense) {  // transpose the frontier to share-column bit rows (not timed as the pull)
             dim3 eg(n_pad / 256u, wact);
@@ -1391,11 +1406,57 @@ int gossip_engine::tick_step_a(int64_t t) {
                                                 d_nz[fcur], ntw, d_FT);
             HIP_TRY(hipGetLastError());
         }
+        // young tiles beside k_pull: the two kernels touch disjoint words; they share the per-node
+        // counters and occupancy words, which k_pull then updates atomically (shared_out) into
+        // occupancy words zeroed here
+        const bool overlap = !dense && ny && opt_young_overlap != 0;
+        if (overlap) {
+            if (!ystream) {
+                HIP_TRY(hipStreamCreateWithFlags(&ystream, hipStreamNonBlocking));
+                HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+                HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+            }
+            HIP_TRY(hipMemsetAsync(d_nz[nxt] + (uint64_t)v0 * ntw, 0, (size_t)(v1 - v0) * ntw * 8u, stream));
+            a.shared_out = 1u;
+        }
         if (cfg.flags & GOSSIP_F_TIMING) {
             e0 = get_event();
             e1 = get_event();
             HIP_TRY(hipEventRecord(e0, stream));
+            if (ny && !dense) {
+                p0 = get_event();
+                HIP_TRY(hipEventRecord(p0, stream));
+            }
         }
+        auto launch_young = [&](hipStream_t ys) -> int {
+            YoungArgs y;
+            y.rowptr = a.rowptr; y.col = a.col; y.deg = d_deg;
+            y.Fcur = d_F[fcur]; y.Fnext = d_F[nxt]; y.seen = d_seen;
+            y.slot_cur = d_slot[fcur]; y.slot_next = d_slot[nxt];
+            y.ctl = d_ctl[slot]; y.wflags = d_wflags[slot];
+            y.recv = d_recv; y.sent = d_sent; y.live = d_live[lv];
+            y.snap = snap_ptr; y.acct = d_acct; y.nz_next = d_nz[nxt]; y.ntw = ntw;
+            y.yt = d_young[slot]->yt; y.ny = ny; y.nr = ny_read; y.nt = ny_leave;
+            y.rmap = d_young[slot]->rmap;
+            y.n = v1; y.v0 = v0; y.stride = stride;
+            y.cap = (uint32_t)std::min<int64_t>(kSlotU16 - 1, std::max<int64_t>(1, opt_young_cap));
+            const uint32_t yg = (uint32_t)std::max<uint64_t>(
+                1, std::min<uint64_t>(((uint64_t)(v1 - v0) + 3) / 4, pull_grid_cap(nt_rows, opt_pull_grid)));
+            hipEvent_t y0 = nullptr, y1 = nullptr;
+            if (cfg.flags & GOSSIP_F_TIMING) {
+                y0 = get_event();
+                y1 = get_event();
+                HIP_TRY(hipEventRecord(y0, ys));
+            }
+            k_pull_young<<<yg, 256, young_lds_bytes(ny, ny_read), ys>>>(y);
+            HIP_TRY(hipGetLastError());
+            if (cfg.flags & GOSSIP_F_TIMING) {
+                HIP_TRY(hipEventRecord(y1, ys));
+                timers_young.emplace_back(y0, y1);
+            }
+            young_launches++;
+            return GOSSIP_OK;
+        };
         if (dense) {
             // The timed kernel in DENSE mode is the MFMA contraction; its incoming words are
             // then consumed by k_pull (dedup/state/counters, untimed).
@@ -1420,38 +1481,34 @@ int gossip_engine::tick_step_a(int64_t t) {
             a.inc = d_inc;
             run_pull(a, false);
         } else {
+            if (overlap) {
+                HIP_TRY(hipEventRecord(ev_fork, stream));
+                HIP_TRY(hipStreamWaitEvent(ystream, ev_fork, 0));
+                if (opt_young_overlap == 1) {
+                    const int rc = launch_young(ystream);
+                    if (rc) return rc;
+                }
+            }
             run_pull(a, true);
             if (cfg.flags & GOSSIP_F_TIMING) {
                 HIP_TRY(hipEventRecord(e1, stream));
                 timers.emplace_back(e0, e1);
             }
-            if (ny) {  // the young tiles (young_kernel.h), after k_pull wrote the nz words
-                YoungArgs y;
-                y.rowptr = a.rowptr; y.col = a.col; y.deg = d_deg;
-                y.Fcur = d_F[fcur]; y.Fnext = d_F[nxt]; y.seen = d_seen;
-                y.slot_cur = d_slot[fcur]; y.slot_next = d_slot[nxt];
-                y.ctl = d_ctl[slot]; y.wflags = d_wflags[slot];
-                y.recv = d_recv; y.sent = d_sent; y.live = d_live[lv];
-                y.snap = snap_ptr; y.acct = d_acct; y.nz_next = d_nz[nxt]; y.ntw = ntw;
-                y.yt = d_young[slot]->yt; y.ny = ny; y.nr = ny_read; y.nt = ny_leave;
-                y.rmap = d_young[slot]->rmap;
-                y.n = v1; y.v0 = v0; y.stride = stride;
-                y.cap = (uint32_t)std::min<int64_t>(kSlotU16 - 1, std::max<int64_t>(1, opt_young_cap));
-                const uint32_t yg = (uint32_t)std::max<uint64_t>(
-                    1, std::min<uint64_t>(((uint64_t)(v1 - v0) + 3) / 4, pull_grid_cap(nt_rows, opt_pull_grid)));
-                hipEvent_t y0 = nullptr, y1 = nullptr;
-                if (cfg.flags & GOSSIP_F_TIMING) {
-                    y0 = get_event();
-                    y1 = get_event();
-                    HIP_TRY(hipEventRecord(y0, stream));
-                }
-                k_pull_young<<<yg, 256, young_lds_bytes(ny, ny_read), stream>>>(y);
-                HIP_TRY(hipGetLastError());
-                if (cfg.flags & GOSSIP_F_TIMING) {
-                    HIP_TRY(hipEventRecord(y1, stream));
-                    timers_young.emplace_back(y0, y1);
-                }
-                young_launches++;
+            if (overlap && opt_young_overlap == 2) {
+                const int rc = launch_young(ystream);
+                if (rc) return rc;
+            }
+            if (overlap) {
+                HIP_TRY(hipEventRecord(ev_join, ystream));
+                HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
+            } else if (ny) {  // the young tiles (young_kernel.h), after k_pull wrote the nz words
+                const int rc = launch_young(stream);
+                if (rc) return rc;
+            }
+            if (ny && (cfg.flags & GOSSIP_F_TIMING)) {  // the whole pull phase
+                p1 = get_event();
+                HIP_TRY(hipEventRecord(p1, stream));
+                timers_phase.emplace_back(p0, p1);
             }
         }
         HIP_TRY(hipGetLastError());
@@ -1822,6 +1879,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_young = env_option("GOSSIP_YOUNG", -1);
         e->opt_young_age = env_option("GOSSIP_YOUNG_AGE", 5);
         e->opt_young_cap = env_option("GOSSIP_YOUNG_CAP", 127);
+        e->opt_young_overlap = env_option("GOSSIP_YOUNG_OVERLAP", 1);
         e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
         e->dense = cfg->mode == GOSSIP_MODE_DENSE;
@@ -2080,6 +2138,9 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     } else if (k == "young_cap") {
         if (value < 1 || value > (int64_t)kSlotU16 - 1) return set_error(GOSSIP_EINVAL, "young_cap: 1 .. 127 entries");
         e->opt_young_cap = value;
+    } else if (k == "young_overlap") {
+        if (value < 0 || value > 2) return set_error(GOSSIP_EINVAL, "young_overlap: 0, 1 or 2");
+        e->opt_young_overlap = value;
     } else if (k == "mem_limit") {
         if (value < 0) return set_error(GOSSIP_EINVAL, "mem_limit >= 0 bytes");
         if (e->have_sched) return set_error(GOSSIP_ESTATE, "mem_limit: set before the schedule");
@@ -2454,6 +2515,17 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
         e->timers_young.clear();
         e->young_ms_done = yms;
         c->young_ms = yms;
+        double pms = e->phase_ms_done;
+        for (auto& p : e->timers_phase) {
+            float x = 0.f;
+            HIP_TRY(hipEventElapsedTime(&x, p.first, p.second));
+            pms += x;
+            e->event_pool.push_back(p.first);
+            e->event_pool.push_back(p.second);
+        }
+        e->timers_phase.clear();
+        e->phase_ms_done = pms;
+        c->pull_phase_ms = pms;
     }
     c->young_launches = e->young_launches;
     c->exchange_bytes_sent = e->exchange_bytes_out;
@@ -2495,6 +2567,12 @@ int gossip_engine_reset_timing(gossip_engine* e) {
     e->timers_young.clear();
     e->young_ms_done = 0.0;
     e->young_launches = 0;
+    for (auto& p : e->timers_phase) {
+        e->event_pool.push_back(p.first);
+        e->event_pool.push_back(p.second);
+    }
+    e->timers_phase.clear();
+    e->phase_ms_done = 0.0;
     if (e->d_acct) {
         HIP_TRY(hipMemsetAsync(e->d_acct, 0, 16 * 8, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));

@@ -384,7 +384,12 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                 nzacc |= nb;
                 const bool last_of_tw = pass + 1u == npass || ((a.wbase + (pass + 1u) * 2u * LPW) >> 10) != tw;
                 if (last_of_tw) {
-                    if (gl == 0 && c0 + idx < n) a.nz_next[(uint64_t)v * a.ntw + tw] = nzacc;
+                    if (gl == 0 && c0 + idx < n) {
+                        if (!a.shared_out)
+                            a.nz_next[(uint64_t)v * a.ntw + tw] = nzacc;
+                        else if (nzacc)
+                            atomicOr(&a.nz_next[(uint64_t)v * a.ntw + tw], nzacc);
+                    }
                     nzacc = 0ull;
                 }
             }
@@ -394,8 +399,13 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
 #pragma unroll
                 for (int off = GRP / 2; off > 0; off >>= 1) c += __shfl_xor(c, off, GRP);
                 if (gl == 0 && c) {
-                    a.recv[v] += c;
-                    a.sent[v] += (uint64_t)c * a.deg[v];
+                    if (a.shared_out) {  // no-return atomics: nothing waits on them
+                        atomicAdd(&a.recv[v], c);
+                        atomicAdd(reinterpret_cast<unsigned long long*>(&a.sent[v]), (unsigned long long)c * a.deg[v]);
+                    } else {
+                        a.recv[v] += c;
+                        a.sent[v] += (uint64_t)c * a.deg[v];
+                    }
                 }
                 cnt = 0;
             }
@@ -627,7 +637,12 @@ __global__ __launch_bounds__(256) void k_pull_wide(PullArgs a) {
                 const uint32_t tw = pw >> 10;
                 nzacc |= (unsigned long long)tiles_any(__ballot(act && ta)) << ((pw >> 4) & 63u);
                 if (pass + 1u == npass || ((pw + 128u) >> 10) != tw) {
-                    if (lane == 0 && v < n) a.nz_next[v * a.ntw + tw] = nzacc;
+                    if (lane == 0 && v < n) {
+                        if (!a.shared_out)
+                            a.nz_next[v * a.ntw + tw] = nzacc;
+                        else if (nzacc)
+                            atomicOr(&a.nz_next[v * a.ntw + tw], nzacc);
+                    }
                     nzacc = 0ull;
                 }
             }
@@ -635,8 +650,13 @@ __global__ __launch_bounds__(256) void k_pull_wide(PullArgs a) {
             if (pass + 1u == npass) {
                 const uint32_t c = (uint32_t)wave_sum((unsigned long long)cnt);
                 if (lane == 0 && c && v < n) {
-                    a.recv[v] += c;
-                    a.sent[v] += (uint64_t)c * a.deg[v];
+                    if (a.shared_out) {
+                        atomicAdd(&a.recv[v], c);
+                        atomicAdd(reinterpret_cast<unsigned long long*>(&a.sent[v]), (unsigned long long)c * a.deg[v]);
+                    } else {
+                        a.recv[v] += c;
+                        a.sent[v] += (uint64_t)c * a.deg[v];
+                    }
                 }
                 cnt = 0;
             }

@@ -149,6 +149,8 @@ def test_c4_sample_matches_oracle_a(gossip, oracle, c4):
         ("auto (young-tile slots on at 10M nodes)", ()),
         ("young tiles off", (("young", 0),)),
         ("young tiles, 8-entry slots (overflow paths at scale)", (("young_cap", 8),)),
+        ("young tiles after k_pull on one stream", (("young_overlap", 0),)),
+        ("young tiles concurrent, k_pull launched first", (("young_overlap", 2),)),
         ("nt rows, 16384-block grid (the C4 production kernel)", (("pull_nt", 1), ("pull_grid", 16384))),
         ("nt rows, 3-block grid", (("pull_nt", 1), ("pull_grid", 3))),
         ("64 word-lanes", (("pull_lpw", 64),)),

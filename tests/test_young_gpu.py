@@ -104,17 +104,21 @@ def test_young_periodic_snapshots(gossip, oracle, monkeypatch):
     assert got == [tuple(x) for x in ref.periodic]
 
 
-def test_young_off_equals_on(gossip):
-    # 200k nodes (below the auto threshold): forced on == forced off, collisions included
+@pytest.mark.parametrize("overlap", [0, 1, 2])
+def test_young_off_equals_on(gossip, overlap):
+    # 200k nodes (below the auto threshold): forced on == forced off, collisions included, with
+    # k_pull_young after k_pull (0) or concurrent on a second stream (1: launched first, 2: second)
     n = 200_000
     topo = gossip.Topology.gnp(n, 16.0 / (n - 1), 79, gossip.TOPO_SKIP, threads=16)
     t_cut = gossip.seconds_to_ns(5.2)
     ev = gossip.make_schedule(n, 80, T0, t_cut, id_mask=0xFFFFF)
     lat = gossip.milliseconds_to_ns(5.0)
-    on = _run(gossip, topo, ev, lat, t_cut, dict(young=1))
+    on = _run(gossip, topo, ev, lat, t_cut, dict(young=1, young_overlap=overlap), flags=gossip.F_TIMING)
     off = _run(gossip, topo, ev, lat, t_cut, dict(young=0))
     a, b = on.stats(), off.stats()
-    assert on.counters().young_launches > 0 and off.counters().young_launches == 0
+    c = on.counters()
+    assert c.young_launches > 0 and off.counters().young_launches == 0
+    assert c.pull_phase_ms > 0
     for k in STATS:
         assert np.array_equal(getattr(a, k), getattr(b, k)), k
     on.close()
