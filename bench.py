@@ -156,7 +156,7 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
         acc["young_sl"] += c1.young_slot_lines
         acc["young_fb"] += c1.young_fallback_rows
         for k in ("young_col_ids", "young_seen_reads", "young_seen_writes", "young_rows_written",
-                  "young_slot_writes"):
+                  "young_slot_writes", "young_line2_misses"):
             acc[k] = acc.get(k, 0) + getattr(c1, k)
         acc["phase_ms"] += c1.pull_phase_ms
         acc["words_hw"] = max(acc["words_hw"], c1.words_hw)
@@ -367,14 +367,16 @@ def main():
                 "achieved": acc["young_bytes"] / yl / (y_ms * 1e6) if y_ms > 0 else None,
                 "slot_lines_per_launch": acc["young_sl"] / yl,
                 "fallback_rows_per_launch": acc["young_fb"] / yl,
+                "second_lines_unhinted_per_launch": acc.get("young_line2_misses", 0) / yl,
                 "bytes_breakdown_per_launch": {
                     "slot_lines_read": 128 * acc["young_sl"] / yl,
                     "fallback_rows_read": 128 * acc["young_fb"] / yl,
-                    "peer_ids": 4 * acc["young_col_ids"] / yl,
+                    "peer_ids_and_hints": 5 * acc["young_col_ids"] / yl,
                     "own_seen_read": 8 * acc["young_seen_reads"] / yl,
                     "own_seen_write": 8 * acc["young_seen_writes"] / yl,
                     "dense_rows_written": 128 * acc["young_rows_written"] / yl,
                     "slot_lines_written": 128 * acc["young_slot_writes"] / yl,
+                    "unhinted_second_lines_read": 128 * acc.get("young_line2_misses", 0) / yl,
                 },
             }
             # wall time of the phase (HIP events around both kernels on the engine stream; they

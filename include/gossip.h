@@ -311,6 +311,7 @@ typedef struct gossip_counters {
     /* wall time of the pull phase (k_pull and k_pull_young, concurrent on two streams when the
      * young_overlap option is on), HIP events on the engine stream (TIMING) */
     double pull_phase_ms;
+    uint64_t young_line2_misses; /* second slot lines fetched without a hint (k_pull_young) */
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 int gossip_engine_reset_timing(gossip_engine* e);

@@ -226,6 +226,11 @@ struct BirthArgs {
     uint32_t cap;              // slot capacity (entries)
     const uint32_t* wt;        // write-sparse index -> tile, this tick
     uint32_t nwt;
+    // a birth that gives its node's slot a second line announces it (young_kernel.h hints)
+    const int64_t* rowptr;
+    const int32_t* rev;
+    uint8_t* hint_next;
+    uint32_t stamp_next;
 };
 
 // Young-tile slot of a birth's node: the arrival bits of the group mask gm in word w (from the
@@ -315,6 +320,12 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
         } else {
             s[1 + hdr] = (uint16_t)((x.widx << 10) | ((w & 15u) << 6) | (x.col & 63u));
             s[0] = (uint16_t)(hdr + 1u);
+            if (1u + hdr == 64u) {  // the first entry of the second line: the rest of it is
+                for (uint32_t k = 65; k < kSlotU16; k++) s[k] = (uint16_t)kSlotTomb;  // tombstones
+                if (a.hint_next)  // and the readers of the next tick load it
+                    for (int64_t j = a.rowptr[v]; j < a.rowptr[v + 1]; j++)
+                        if (a.rev[j] >= 0) a.hint_next[a.rev[j]] = (uint8_t)a.stamp_next;
+            }
         }
         *sp |= bit;
         a.effgen[v] += 1u;
@@ -428,12 +439,14 @@ struct Instance {
 struct YoungPack {
     YoungTile yt[kYoungMax];  // k_pull_young's tiles, sorted by tile
     uint32_t wt[64];          // write-sparse index -> tile (births, spills)
-    uint8_t rmap[64];         // F_cur entry index -> position in yt (0xff: not read)
+    uint8_t lv[kYoungMax];    // positions in yt of the leaving tiles, by tile
 };
 
 constexpr int kRing = 4;   // host staging slots
 constexpr int kLag = 2;    // ticks of lag before liveness is read back
 constexpr uint32_t kTileWords = 16;  // allocation unit: 16 words = 1024 shares = 128 B per row
+// second-line hint stamp of tick t (young_kernel.h): never 0, the value hint bytes start with
+inline uint32_t hint_stamp(int64_t t) { return 1u + (uint32_t)(((t % 255) + 255) % 255); }
 
 }  // namespace
 
@@ -553,7 +566,8 @@ struct gossip_engine {
     int64_t opt_young = -1;           // young tiles (k_pull_young): -1 auto, 0 off, 1 on
     int64_t opt_young_age = 5;        // write-sparse while the oldest shares are <= this many hops
     int64_t opt_young_cap = 127;      // slot entries per node before it overflows to dense rows
-    int64_t opt_young_overlap = 1;    // k_pull_young beside k_pull on a second stream (1, 2) or after (0)
+    int64_t opt_young_overlap = 1;    // k_pull_young beside k_pull on a second stream (1-4) or after (0)
+    int64_t opt_young_grid = 0;       // k_pull_young blocks, 0 = the pull grid
     hipStream_t ystream = nullptr;    // the second stream (created on first use)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers_phase;  // pull phase (both kernels)
@@ -563,6 +577,8 @@ struct gossip_engine {
     // ---- young tiles (young_kernel.h)
     bool young = false;
     uint16_t* d_slot[2] = {nullptr, nullptr};  // per frontier buffer: n x kSlotU16
+    int32_t* d_rev = nullptr;                   // CSR entry of the reverse edge (-1: none)
+    uint8_t* d_hint[2] = {nullptr, nullptr};    // per frontier buffer: second-line hints per entry
     std::vector<int64_t> tile_first;           // tick of a tile's first birth
     std::vector<uint8_t> tile_widx;            // write-sparse index of the last tick (0xff: none)
     std::vector<uint32_t> wt_last;             // write-sparse index -> tile of the last tick
@@ -634,6 +650,7 @@ gossip_engine::~gossip_engine() {
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     hipFree(d_msg); hipFree(d_cnt); hipFree(d_scan_tmp); hipFree(d_recv_msgs); hipFree(d_sizes);
     hipFree(d_slot[0]); hipFree(d_slot[1]);
+    hipFree(d_rev); hipFree(d_hint[0]); hipFree(d_hint[1]);
     for (int k = 0; k < kRing; k++) { hipFree(d_young[k]); hipHostFree(h_young[k]); }
     for (auto& p : timers_young) {
         hipEventDestroy(p.first);
@@ -840,13 +857,15 @@ int gossip_engine::alloc_device() {
     stride = (words + kTileWords - 1) / kTileWords * kTileWords;  // rows start on 128-B lines
     // Young tiles: the CSR tick pull on graphs whose frontier rows outgrow the caches (C3/C4).
     {
-        const bool ok = !dense && !batch && !handshake && row_count == 1 && !(cfg.flags & GOSSIP_F_NOSKIP);
+        const bool ok = !dense && !batch && !handshake && row_count == 1 && !(cfg.flags & GOSSIP_F_NOSKIP) &&
+                        n < (1u << 31);  // (peer ids carry a hint in bit 31)
         if (opt_young == 1 && !ok)
             return set_error(GOSSIP_EINVAL, "young tiles need the CSR tick engine (not DENSE, HOP_BATCH, "
                                             "HANDSHAKE, NOSKIP or a row partition)");
         young = ok && (opt_young == 1 || (opt_young == -1 && n >= (1u << 20)));
     }
-    const uint64_t slot_bytes = young ? 2ull * n * kSlotU16 * 2u : 0ull;
+    // slots, plus the second-line hints (young_kernel.h): reverse-edge index + 2 hint bytes per entry
+    const uint64_t slot_bytes = young ? 2ull * n * kSlotU16 * 2u + nnz * 6u : 0ull;
     size_t freeb = 0, totalb = 0;
     HIP_TRY(hipMemGetInfo(&freeb, &totalb));
     if (opt_mem_limit > 0) {  // a memory budget below the device's (tests, co-located engines)
@@ -909,8 +928,37 @@ int gossip_engine::alloc_device() {
     HIP_TRY(hipMemsetAsync(d_acct, 0, 16 * 8, stream));
     if (young) {
         for (int k = 0; k < 2; k++) {
+            // empty slots: header 0, every entry a tombstone (readers scatter whole lines)
             HIP_TRY(hipMalloc(&d_slot[k], (size_t)n * kSlotU16 * 2u));
-            HIP_TRY(hipMemsetAsync(d_slot[k], 0, (size_t)n * kSlotU16 * 2u, stream));
+            HIP_TRY(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(d_slot[k]), (unsigned short)kSlotTomb,
+                                      (size_t)n * kSlotU16, stream));
+            HIP_TRY(hipMemset2DAsync(d_slot[k], kSlotU16 * 2u, 0, 2, n, stream));
+            HIP_TRY(hipMalloc(&d_hint[k], std::max<size_t>(nnz, 1)));
+            HIP_TRY(hipMemsetAsync(d_hint[k], 0, std::max<size_t>(nnz, 1), stream));  // stamps are >= 1
+        }
+        {  // reverse edges: rev[j] = the entry of v in the list of u = col[j] (j in v's list)
+            std::vector<int32_t> rev(nnz, -1), perm(nnz);
+            const int th = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+            gossip::parallel_for(n, th, [&](uint64_t lo, uint64_t hi) {  // each row's entries by id
+                for (uint64_t u = lo; u < hi; u++) {
+                    const int64_t b = h_rowptr[u], e = h_rowptr[u + 1];
+                    for (int64_t j = b; j < e; j++) perm[j] = (int32_t)j;
+                    std::sort(perm.begin() + b, perm.begin() + e,
+                              [&](int32_t x, int32_t y) { return h_col[x] < h_col[y]; });
+                }
+            });
+            gossip::parallel_for(n, th, [&](uint64_t lo, uint64_t hi) {
+                for (uint64_t v = lo; v < hi; v++)
+                    for (int64_t j = h_rowptr[v]; j < h_rowptr[v + 1]; j++) {
+                        const uint32_t u = (uint32_t)h_col[j];
+                        auto b = perm.begin() + h_rowptr[u], e = perm.begin() + h_rowptr[u + 1];
+                        auto it = std::lower_bound(b, e, (int32_t)v,
+                                                   [&](int32_t x, int32_t val) { return h_col[x] < val; });
+                        if (it != e && (uint32_t)h_col[*it] == v) rev[j] = *it;
+                    }
+            });
+            HIP_TRY(hipMalloc(&d_rev, std::max<size_t>(nnz, 1) * 4));
+            if (nnz) HIP_TRY(hipMemcpy(d_rev, rev.data(), nnz * 4, hipMemcpyHostToDevice));
         }
         for (int k = 0; k < kRing; k++) {
             HIP_TRY(hipMalloc(&d_young[k], sizeof(YoungPack)));
@@ -1244,7 +1292,11 @@ int gossip_engine::tick_step_a(int64_t t) {
             return a.first != b.first ? a.first > b.first : a.tile < b.tile;  // youngest first
         });
         new_widx.assign(tile_widx.size(), 0xffu);
-        std::fill(YP->rmap, YP->rmap + 64, (uint8_t)0xffu);
+        // read tiles sit at their F_cur entry index (young_kernel.h): nr = last tick's write count
+        ny_read = (uint32_t)wt_last.size();
+        for (uint32_t r = 0; r < ny_read; r++) YP->yt[r] = YoungTile{wt_last[r], 0u, (uint8_t)r, 0xffu, 0};
+        uint32_t nfresh = 0;
+        YoungTile fresh[kYoungMax];
         uint32_t fresh_room = kYoungMax > nrd ? kYoungMax - nrd : 0u;  // nrd <= kYoungWriteMax < kYoungMax
         for (const Cand& c : cand) {
             const bool wr_age = t + 1 - c.first <= opt_young_age && nwt < kYoungWriteMax;
@@ -1259,21 +1311,17 @@ int gossip_engine::tick_step_a(int64_t t) {
                 YP->wt[nwt++] = c.tile;
                 new_widx[c.tile] = y.w_idx;
             }
-            YP->yt[ny++] = y;
+            if (c.rd)
+                YP->yt[y.r_idx] = y;  // (a read tile whose tile is gone keeps flags 0: no output)
+            else
+                fresh[nfresh++] = y;
         }
-        // order (young_kernel.h): leaving tiles, staying read tiles, fresh tiles; each by tile
-        auto part = [](const YoungTile& y) {
-            return (y.flags & YT_READ) ? ((y.flags & YT_WRITE) ? 1 : 0) : 2;
-        };
-        std::sort(YP->yt, YP->yt + ny, [&](const YoungTile& a, const YoungTile& b) {
-            return part(a) != part(b) ? part(a) < part(b) : a.tile < b.tile;
-        });
-        for (uint32_t i = 0; i < ny; i++) {
-            const int pt = part(YP->yt[i]);
-            ny_leave += pt == 0;
-            ny_read += pt <= 1;
-            if (YP->yt[i].flags & YT_READ) YP->rmap[YP->yt[i].r_idx] = (uint8_t)i;
-        }
+        std::sort(fresh, fresh + nfresh, [](const YoungTile& a, const YoungTile& b) { return a.tile < b.tile; });
+        for (uint32_t k = 0; k < nfresh; k++) YP->yt[ny_read + k] = fresh[k];
+        ny = ny_read + nfresh;
+        for (uint32_t r = 0; r < ny_read; r++)
+            if (YP->yt[r].flags == YT_READ) YP->lv[ny_leave++] = (uint8_t)r;
+        std::sort(YP->lv, YP->lv + ny_leave, [&](uint8_t a, uint8_t b) { return YP->yt[a].tile < YP->yt[b].tile; });
         for (uint32_t q = 0; q < nb; q++) {
             const uint32_t tl = B[q].col >> 10;
             B[q].widx = tl < new_widx.size() ? new_widx[tl] : 0xffu;
@@ -1330,7 +1378,8 @@ int gossip_engine::tick_step_a(int64_t t) {
                           (c.keep != ~0ull ? WF_KEEP : 0u) | (c.snap ? WF_SNAP : 0u));
     }
     for (uint32_t i = 0; i < ny; i++)  // k_pull leaves these words to k_pull_young
-        for (uint32_t q = 0; q < kTileWords; q++) WF[YP->yt[i].tile * kTileWords + q] |= (uint8_t)WF_YOUNG;
+        if (YP->yt[i].flags)
+            for (uint32_t q = 0; q < kTileWords; q++) WF[YP->yt[i].tile * kTileWords + q] |= (uint8_t)WF_YOUNG;
     for (uint32_t w : reset_now) ctl[w].clear = 0ull;
     // 5. upload + launches
     const uint32_t wact = hw;
@@ -1412,7 +1461,11 @@ int gossip_engine::tick_step_a(int64_t t) {
         const bool overlap = !dense && ny && opt_young_overlap != 0;
         if (overlap) {
             if (!ystream) {
-                HIP_TRY(hipStreamCreateWithFlags(&ystream, hipStreamNonBlocking));
+                // young_overlap 3 / 4: the second stream at the lowest / highest priority
+                int lo = 0, hi = 0;
+                HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+                const int prio = opt_young_overlap == 3 ? lo : opt_young_overlap == 4 ? hi : 0;
+                HIP_TRY(hipStreamCreateWithPriority(&ystream, hipStreamNonBlocking, prio));
                 HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
                 HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
             }
@@ -1437,11 +1490,14 @@ int gossip_engine::tick_step_a(int64_t t) {
             y.recv = d_recv; y.sent = d_sent; y.live = d_live[lv];
             y.snap = snap_ptr; y.acct = d_acct; y.nz_next = d_nz[nxt]; y.ntw = ntw;
             y.yt = d_young[slot]->yt; y.ny = ny; y.nr = ny_read; y.nt = ny_leave;
-            y.rmap = d_young[slot]->rmap;
+            y.lv = d_young[slot]->lv;
             y.n = v1; y.v0 = v0; y.stride = stride;
             y.cap = (uint32_t)std::min<int64_t>(kSlotU16 - 1, std::max<int64_t>(1, opt_young_cap));
+            y.hint_cur = d_hint[fcur]; y.hint_next = d_hint[nxt]; y.rev = d_rev;
+            y.stamp_cur = hint_stamp(t - 1); y.stamp_next = hint_stamp(t);
             const uint32_t yg = (uint32_t)std::max<uint64_t>(
-                1, std::min<uint64_t>(((uint64_t)(v1 - v0) + 3) / 4, pull_grid_cap(nt_rows, opt_pull_grid)));
+                1, std::min<uint64_t>(((uint64_t)(v1 - v0) + 3) / 4,
+                                      opt_young_grid > 0 ? (uint64_t)opt_young_grid : pull_grid_cap(nt_rows, opt_pull_grid)));
             hipEvent_t y0 = nullptr, y1 = nullptr;
             if (cfg.flags & GOSSIP_F_TIMING) {
                 y0 = get_event();
@@ -1484,7 +1540,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             if (overlap) {
                 HIP_TRY(hipEventRecord(ev_fork, stream));
                 HIP_TRY(hipStreamWaitEvent(ystream, ev_fork, 0));
-                if (opt_young_overlap == 1) {
+                if (opt_young_overlap != 2) {
                     const int rc = launch_young(ystream);
                     if (rc) return rc;
                 }
@@ -1528,6 +1584,9 @@ int gossip_engine::tick_step_a(int64_t t) {
         b.cap = (uint32_t)std::min<int64_t>(kSlotU16 - 1, std::max<int64_t>(1, opt_young_cap));
         b.wt = young ? d_young[slot]->wt : nullptr;
         b.nwt = nwt;
+        b.rowptr = d_rowptr; b.rev = d_rev;
+        b.hint_next = young ? d_hint[nxt] : nullptr;
+        b.stamp_next = hint_stamp(t);
         k_births<<<(nb + 255) / 256, 256, 0, stream>>>(b);
         HIP_TRY(hipGetLastError());
     }
@@ -1880,6 +1939,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_young_age = env_option("GOSSIP_YOUNG_AGE", 5);
         e->opt_young_cap = env_option("GOSSIP_YOUNG_CAP", 127);
         e->opt_young_overlap = env_option("GOSSIP_YOUNG_OVERLAP", 1);
+        e->opt_young_grid = env_option("GOSSIP_YOUNG_GRID", 0);
         e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
         e->dense = cfg->mode == GOSSIP_MODE_DENSE;
@@ -2139,8 +2199,11 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
         if (value < 1 || value > (int64_t)kSlotU16 - 1) return set_error(GOSSIP_EINVAL, "young_cap: 1 .. 127 entries");
         e->opt_young_cap = value;
     } else if (k == "young_overlap") {
-        if (value < 0 || value > 2) return set_error(GOSSIP_EINVAL, "young_overlap: 0, 1 or 2");
+        if (value < 0 || value > 4) return set_error(GOSSIP_EINVAL, "young_overlap: 0 .. 4");
         e->opt_young_overlap = value;
+    } else if (k == "young_grid") {
+        if (value < 0 || value > (1 << 20)) return set_error(GOSSIP_EINVAL, "young_grid: 0 .. 2^20 blocks");
+        e->opt_young_grid = value;
     } else if (k == "mem_limit") {
         if (value < 0) return set_error(GOSSIP_EINVAL, "mem_limit >= 0 bytes");
         if (e->have_sched) return set_error(GOSSIP_ESTATE, "mem_limit: set before the schedule");
@@ -2538,8 +2601,10 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     c->young_rows_written = acct[13];
     c->young_slot_writes = acct[14];
     // k_pull_young's bytes: 128 B per slot line / fallback row / row written / slot written,
-    // 4 B per peer id, 8 B per own seen word, row_ptr + counters per node and launch
-    c->young_bytes_moved = 128ull * (acct[8] + acct[10] + acct[13] + acct[14]) + 4ull * acct[9] +
+    // 5 B per peer (id + second-line hint), 8 B per own seen word, row_ptr + counters per node
+    // and launch
+    c->young_line2_misses = acct[15];
+    c->young_bytes_moved = 128ull * (acct[8] + acct[10] + acct[13] + acct[14] + acct[15]) + 5ull * acct[9] +
                            8ull * (acct[11] + acct[12]) + e->young_launches * (8ull * (e->n + 1) + 16ull * e->n);
     uint64_t g = 0;
     const uint64_t done = (uint64_t)std::max<int64_t>(0, std::min(e->cur, e->tick_end) - e->tick0);

@@ -50,9 +50,12 @@ struct YoungTile {
     uint8_t pad;
 };
 
-// yt order (host): [0, nt) read-sparse tiles leaving the young set (dense output), [nt, nr)
-// read-sparse tiles staying young, [nr, ny) fresh write-sparse tiles (no input); each part sorted
-// by tile.  Accumulators exist for the nr read tiles only.
+// yt order (host): [0, nr) the read-sparse tiles BY THEIR INDEX IN F_cur's ENTRIES (so an entry
+// (r << 10) | (word << 6) | bit lands in accumulator word (r << 4) | word = entry >> 6, with no
+// lookup), then [nr, ny) the fresh write-sparse tiles (no input).  A read tile is leaving
+// (YT_READ only: dense output) or staying (YT_READ | YT_WRITE); lv[0, nt) lists the leaving
+// positions by tile.  Every unused entry of a written slot line is a tombstone, so readers
+// scatter whole lines without looking at the count (tombstones land in spare words).
 struct YoungArgs {
     const int64_t* rowptr;
     const int32_t* col;
@@ -73,14 +76,26 @@ struct YoungArgs {
     uint32_t ntw;
     const YoungTile* yt;
     uint32_t ny, nr, nt;
-    const uint8_t* rmap;  // [64] w_idx of F_cur entries -> position in yt (< nr; 0xff: not read)
+    const uint8_t* lv;  // [nt] positions in yt of the leaving tiles, by tile
     uint32_t n, v0, stride, cap;
+    // Second-line hints (per CSR entry): hint_cur[j] == stamp_cur says that the slot of peer
+    // col[j] holds more than 63 entries this tick, so its second line is loaded together with the
+    // first; a writer with a two-line slot marks every reverse entry rev[j] of its own list in
+    // hint_next with stamp_next.  A hint is only a hint: a peer whose header says two lines
+    // without one is fetched on demand (acct[15]).
+    const uint8_t* hint_cur;
+    uint8_t* hint_next;
+    const int32_t* rev;
+    uint32_t stamp_cur, stamp_next;
 };
 
+constexpr uint32_t kYoungSpare = 32;  // spare accumulator words per wave (tombstones land here)
+
 __host__ __device__ constexpr size_t young_lds_bytes(uint32_t ny, uint32_t nr) {
-    // 4 waves x (accumulator 8 B + touched list 2 B per read word + a slot staging buffer),
-    // tiles, read-word flags, rmap
-    return (size_t)nr * 16u * 10u * 4u + 4u * kSlotU16 * 2u + (size_t)ny * sizeof(YoungTile) + (size_t)nr * 16u + 64u;
+    // 4 waves x (accumulator 8 B per read word + spares, touched list 2 B per read word, a slot
+    // staging buffer), tiles, read-word flags, leaving positions
+    return 4u * ((size_t)nr * 16u + kYoungSpare) * 8u + 4u * (size_t)nr * 16u * 2u + 4u * kSlotU16 * 2u +
+           (size_t)ny * sizeof(YoungTile) + (size_t)nr * 16u + 64u;
 }
 
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane) {
@@ -106,34 +121,39 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m, uint32_t l
 __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
     extern __shared__ unsigned long long smem[];
     const uint32_t nrw = a.nr * 16u;  // accumulated words
+    const uint32_t accw = nrw + kYoungSpare;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    unsigned long long* s_acc = smem + wv * nrw;
-    uint16_t* s_list = reinterpret_cast<uint16_t*>(smem + 4u * nrw) + wv * nrw;
-    uint16_t* s_out = reinterpret_cast<uint16_t*>(smem + 4u * nrw) + 4u * nrw + wv * kSlotU16;  // 16-B aligned
-    YoungTile* s_yt = reinterpret_cast<YoungTile*>(reinterpret_cast<uint16_t*>(smem + 4u * nrw) + 4u * nrw + 4u * kSlotU16);
+    unsigned long long* s_acc = smem + wv * accw;
+    uint16_t* s_list = reinterpret_cast<uint16_t*>(smem + 4u * accw) + wv * nrw;
+    uint16_t* s_out = reinterpret_cast<uint16_t*>(smem + 4u * accw) + 4u * nrw + wv * kSlotU16;  // 16-B aligned
+    YoungTile* s_yt = reinterpret_cast<YoungTile*>(reinterpret_cast<uint16_t*>(smem + 4u * accw) + 4u * nrw + 4u * kSlotU16);
     uint8_t* s_wf = reinterpret_cast<uint8_t*>(s_yt + a.ny);
-    uint8_t* s_rmap = s_wf + nrw;
+    uint8_t* s_lv = s_wf + nrw;
     for (uint32_t i = threadIdx.x; i < a.ny; i += 256) s_yt[i] = a.yt[i];
-    if (threadIdx.x < 64) s_rmap[threadIdx.x] = a.rmap[threadIdx.x];
+    if (threadIdx.x < a.nt) s_lv[threadIdx.x] = a.lv[threadIdx.x];
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nrw; i += 256) s_wf[i] = a.wflags[s_yt[i >> 4].tile * 16u + (i & 15u)];
-    for (uint32_t i = lane; i < nrw; i += 64) s_acc[i] = 0ull;
+    for (uint32_t i = lane; i < accw; i += 64) s_acc[i] = 0ull;
     if (blockIdx.x == 0)  // young tiles are alive by definition (see above)
-        for (uint32_t i = threadIdx.x; i < a.ny * 16u; i += 256) a.live[s_yt[i >> 4].tile * 16u + (i & 15u)] = ~0ull;
+        for (uint32_t i = threadIdx.x; i < a.ny * 16u; i += 256)
+            if (s_yt[i >> 4].flags) a.live[s_yt[i >> 4].tile * 16u + (i & 15u)] = ~0ull;
     __syncthreads();
     const uint64_t wave = (uint64_t)blockIdx.x * 4u + wv;
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t stride = a.stride;
     unsigned long long snap_local = 0ull;
     // traffic (wave-uniform): slot lines, peer ids, dense fallback rows, seen r/w, row/slot writes
-    uint32_t t_sl = 0, t_col = 0, t_fb = 0, t_srd = 0, t_swr = 0, t_rw = 0, t_slw = 0;
+    uint32_t t_sl = 0, t_col = 0, t_fb = 0, t_srd = 0, t_swr = 0, t_rw = 0, t_slw = 0, t_miss = 0;
 
-    auto scatter = [&](uint32_t e) {
-        if (e == kSlotTomb) return;
-        const uint32_t pos = s_rmap[e >> 10];
-        if (pos == 0xffu) return;
-        const uint32_t b = e & 1023u;
-        atomicOr(&s_acc[pos * 16u + (b >> 6)], 1ull << (b & 63u));
+    // the 8 entries of a lane's 16-B piece of a slot line; `hdr`: entry 0 is the line's header
+    const uint32_t spare = nrw + (lane & (kYoungSpare - 1u));
+    auto scatter8 = [&](const ulonglong2& q, bool hdr) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t e = (j == 0 && hdr) ? kSlotTomb : slot_entry(q, j);
+            const uint32_t w = e >> 6;
+            atomicOr(&s_acc[w < nrw ? w : spare], 1ull << (e & 63u));
+        }
     };
 
     for (uint64_t c0 = a.v0 + wave * 64u; c0 < a.n; c0 += nwaves * 64u) {
@@ -141,11 +161,14 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
         const int64_t rp = a.rowptr[c0 + min(lane, cnt_nodes)];
         const int64_t rp_end = a.rowptr[c0 + cnt_nodes];
         // peer ids of node j (lane p = peer p of its first 64), one node ahead of the gather
+        // (the peer's id, and bit 31: its slot has a second line -- ids are < 2^31)
         auto load_ids = [&](uint32_t j) -> uint32_t {
             const int32_t b = __shfl((int)rp, (int)(j & 63u), 64);
             const int32_t nx = __shfl((int)rp, (int)((j + 1u) & 63u), 64);
             const int32_t e = j + 1u < 64u ? nx : (int32_t)rp_end;
-            return j < cnt_nodes && (int32_t)lane < e - b ? (uint32_t)a.col[b + (int32_t)lane] : 0xffffffffu;
+            if (!(j < cnt_nodes && (int32_t)lane < e - b)) return 0xffffffffu;
+            const uint32_t id = (uint32_t)a.col[b + (int32_t)lane];
+            return a.hint_cur[b + (int32_t)lane] == a.stamp_cur ? id | 0x80000000u : id;
         };
         uint32_t cid_cur = load_ids(0u);
         for (uint32_t jn = 0; jn < cnt_nodes; jn++) {
@@ -157,41 +180,47 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
             // ---- gather: peers' whole slots (both lines) -> accumulator ----
             for (int32_t cb = beg; cb < end; cb += 64) {
                 const int32_t np = min(64, end - cb);
-                const uint32_t cid = cb == beg ? cid_cur
-                                               : ((int32_t)lane < np ? (uint32_t)a.col[cb + (int32_t)lane] : 0xffffffffu);
+                uint32_t cid = cid_cur;
+                if (cb != beg) {  // peers beyond the first 64 (rare): loaded here
+                    cid = 0xffffffffu;
+                    if ((int32_t)lane < np) {
+                        cid = (uint32_t)a.col[cb + (int32_t)lane];
+                        if (a.hint_cur[cb + (int32_t)lane] == a.stamp_cur) cid |= 0x80000000u;
+                    }
+                }
                 t_col += (uint32_t)np;
                 unsigned long long ovf = 0ull;  // bit p: peer cb+p
                 for (int32_t pb = 0; pb < np; pb += 8 * kYoungQ) {
                     ulonglong2 q[kYoungQ], q2[kYoungQ];
+                    uint32_t missk = 0u;  // bit k: group k's peer has a second line nobody announced
 #pragma unroll
                     for (int k = 0; k < kYoungQ; k++) {
                         const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
                         const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64);
-                        q[k] = q2[k] = make_ulonglong2(0ull, 0ull);
+                        q[k] = make_ulonglong2(~0ull, ~0ull);  // tombstones: nothing to scatter
+                        q2[k] = make_ulonglong2(~0ull, ~0ull);
                         if (p < 64u && u != 0xffffffffu) {
-                            const uint16_t* sl = a.slot_cur + (uint64_t)u * kSlotU16 + (lane & 7u) * 8u;
+                            const uint16_t* sl = a.slot_cur + (uint64_t)(u & 0x7fffffffu) * kSlotU16 + (lane & 7u) * 8u;
                             q[k] = *reinterpret_cast<const ulonglong2*>(sl);
-                            q2[k] = *reinterpret_cast<const ulonglong2*>(sl + 64u);
+                            if (u & 0x80000000u) q2[k] = *reinterpret_cast<const ulonglong2*>(sl + 64u);
                         }
                     }
 #pragma unroll
                     for (int k = 0; k < kYoungQ; k++) {
                         if (pb + k * 8 >= np) break;  // (uniform) no peer in this group of 8
                         const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
-                        const bool valid = p < 64u && (uint32_t)__shfl((int)cid, (int)(p & 63u), 64) != 0xffffffffu;
-                        const uint32_t hdr = (uint32_t)__shfl((int)(q[k].x & 0xffffull), (int)(lane & ~7u), 64);
-                        t_sl += wave_count(valid && (lane & 7u) == 0u) * 2u;
-                        const bool ok = valid && hdr != kSlotOverflow;
-                        const uint32_t lim = ok ? hdr : 0u;
-#pragma unroll
-                        for (int j = 0; j < 8; j++) {
-                            const uint32_t pos = (lane & 7u) * 8u + (uint32_t)j;
-                            if (pos >= 1u && pos <= lim) scatter(slot_entry(q[k], j));
-                        }
-                        if (__ballot(lim > 63u)) {  // (uniform) some peer has a second line
-#pragma unroll
-                            for (int j = 0; j < 8; j++)
-                                if (64u + (lane & 7u) * 8u + (uint32_t)j <= lim) scatter(slot_entry(q2[k], j));
+                        const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64);
+                        const bool valid = p < 64u && u != 0xffffffffu;
+                        const bool hinted = valid && (u & 0x80000000u);
+                        const uint32_t hdr = valid ? (uint32_t)__shfl((int)(q[k].x & 0xffffull), (int)(lane & ~7u), 64) : 0u;
+                        t_sl += wave_count(valid && (lane & 7u) == 0u) + wave_count(hinted && (lane & 7u) == 0u);
+                        // an overflowed slot's entries are a subset of its dense rows (read below)
+                        scatter8(q[k], (lane & 7u) == 0u);
+                        const bool two = hdr != kSlotOverflow && hdr > 63u;
+                        if (__ballot(two || hinted)) {  // (uniform) some second line in this group
+                            if (two && !hinted) missk |= 1u << k;  // fetched after the batch
+                            if (!two) q2[k] = make_ulonglong2(~0ull, ~0ull);  // stale hint
+                            scatter8(q2[k], false);
                         }
                         const unsigned long long mo = __ballot((lane & 7u) == 0u && valid && hdr == kSlotOverflow);
                         if (mo) {
@@ -200,12 +229,25 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
                                 if ((mo >> (8 * g)) & 1ull) ovf |= 1ull << (((uint32_t)pb + (uint32_t)k * 8u + (uint32_t)g) & 63u);
                         }
                     }
+                    if (__ballot(missk != 0u)) {  // (uniform, rare) unannounced second lines
+                        for (int k = 0; k < kYoungQ; k++) {
+                            const bool miss = (missk >> k) & 1u;
+                            if (!__ballot(miss)) continue;
+                            const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
+                            const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64) & 0x7fffffffu;
+                            ulonglong2 x = make_ulonglong2(~0ull, ~0ull);
+                            if (miss) x = *reinterpret_cast<const ulonglong2*>(a.slot_cur + (uint64_t)u * kSlotU16 + 64u + (lane & 7u) * 8u);
+                            t_miss += wave_count(miss && (lane & 7u) == 0u);
+                            scatter8(x, false);
+                        }
+                    }
                 }
                 while (ovf) {  // overflowed peers: their dense rows of every read-sparse tile
                     const int p = __builtin_ctzll(ovf);
                     ovf &= ovf - 1ull;
-                    const uint32_t u = (uint32_t)__shfl((int)cid, p, 64);
+                    const uint32_t u = (uint32_t)__shfl((int)cid, p, 64) & 0x7fffffffu;
                     for (uint32_t i = lane; i < nrw; i += 64) {
+                        if (!s_yt[i >> 4].flags) continue;  // a position whose tile is gone
                         const uint64_t x = a.Fcur[(uint64_t)u * stride + s_yt[i >> 4].tile * 16u + (i & 15u)];
                         if (x) s_acc[i] |= x;  // this lane owns word i here
                     }
@@ -265,7 +307,10 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
             const uint32_t total = (uint32_t)wave_sum((unsigned long long)cnt_sp);
             const bool overflow = total > a.cap;
             uint16_t* out = a.slot_next + v * kSlotU16;
-            // the slot is staged in LDS and written as whole lines (no partial-line writes)
+            // the slot is staged in LDS and written as whole lines (no partial-line writes); every
+            // unused entry is a tombstone (readers scatter whole lines)
+            reinterpret_cast<uint32_t*>(s_out)[lane] = 0xffffffffu;
+            __builtin_amdgcn_wave_barrier();
             if (!overflow && total) {
                 uint32_t base = 1;
                 for (uint32_t t0 = 0; t0 < ntouch; t0 += 64) {
@@ -290,16 +335,23 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
                 if (lane < 8u * lines)
                     *reinterpret_cast<ulonglong2*>(out + lane * 8u) = *reinterpret_cast<const ulonglong2*>(s_out + lane * 8u);
                 t_slw += lines;
+                if (lines == 2u)  // announce the second line to the readers of the next tick
+                    for (int32_t j = beg + (int32_t)lane; j < end; j += 64) {
+                        const int32_t r = a.rev[j];
+                        if (r >= 0) a.hint_next[r] = (uint8_t)a.stamp_next;
+                    }
             }
-            // dense rows: the leaving tiles [0, nt) always; every write-sparse tile if overflowed
+            // dense rows: the leaving tiles (lv) always; every position if overflowed (leaving and
+            // write-sparse tiles get rows)
             const uint32_t ndense = overflow ? a.ny : a.nt;
             unsigned long long nzw = 0ull;
             uint32_t nz_tw = 0xffffffffu;
             for (uint32_t q0 = 0; q0 < ndense; q0 += 4) {
-                const uint32_t q = q0 + (lane >> 4), word = lane & 15u;
-                const bool in = q < ndense;
-                const YoungTile yt = s_yt[in ? q : 0u];
-                const bool leaving = in && q < a.nt;
+                const uint32_t qi = q0 + (lane >> 4), word = lane & 15u;
+                const bool in = qi < ndense;
+                const uint32_t q = !in ? 0u : overflow ? qi : (uint32_t)s_lv[qi];
+                const YoungTile yt = s_yt[q];
+                const bool leaving = in && (yt.flags & (YT_READ | YT_WRITE)) == YT_READ;
                 const bool dense_out = leaving || (in && (yt.flags & YT_WRITE));
                 const uint64_t x = (in && q < a.nr) ? s_acc[q * 16u + word] : 0ull;
                 const unsigned long long m = __ballot(in && x != 0ull);
@@ -340,9 +392,9 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
         if (lane == 0 && snap_local) atomicAdd(a.snap, snap_local);
     }
     if (a.acct && lane == 0) {
-        const uint32_t tv[7] = {t_sl, t_col, t_fb, t_srd, t_swr, t_rw, t_slw};
+        const uint32_t tv[8] = {t_sl, t_col, t_fb, t_srd, t_swr, t_rw, t_slw, t_miss};
 #pragma unroll
-        for (int q = 0; q < 7; q++)
+        for (int q = 0; q < 8; q++)
             if (tv[q]) atomicAdd(&a.acct[8 + q], (unsigned long long)tv[q]);
     }
 }

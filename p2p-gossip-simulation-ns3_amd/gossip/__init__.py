@@ -104,7 +104,7 @@ class gossip_counters(C.Structure):
         ("young_seen_reads", C.c_uint64), ("young_seen_writes", C.c_uint64),
         ("young_rows_written", C.c_uint64), ("young_slot_writes", C.c_uint64),
         ("exchange_bytes_sent", C.c_uint64), ("exchange_bytes_received", C.c_uint64),
-        ("pull_phase_ms", C.c_double),
+        ("pull_phase_ms", C.c_double), ("young_line2_misses", C.c_uint64),
     ]
 
 
