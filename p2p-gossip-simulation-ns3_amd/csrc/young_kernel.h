@@ -151,8 +151,8 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const uint32_t e = (j == 0 && hdr) ? kSlotTomb : slot_entry(q, j);
-            const uint32_t w = e >> 6;
-            atomicOr(&s_acc[w < nrw ? w : spare], 1ull << (e & 63u));
+            // (w >= nrw lands in [nrw, spare] -- the spare words)
+            atomicOr(&s_acc[min(e >> 6, spare)], 1ull << (e & 63u));
         }
     };
 
@@ -161,87 +161,87 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
         const int64_t rp = a.rowptr[c0 + min(lane, cnt_nodes)];
         const int64_t rp_end = a.rowptr[c0 + cnt_nodes];
         // peer ids of node j (lane p = peer p of its first 64), one node ahead of the gather
-        // (the peer's id, and bit 31: its slot has a second line -- ids are < 2^31)
-        auto load_ids = [&](uint32_t j) -> uint32_t {
+        // (the peer's id and its hint byte, combined only when the node's gather starts: bit 31
+        // of the id says the peer's slot has a second line -- ids are < 2^31)
+        auto load_ids = [&](uint32_t j, uint32_t& hint) -> uint32_t {
             const int32_t b = __shfl((int)rp, (int)(j & 63u), 64);
             const int32_t nx = __shfl((int)rp, (int)((j + 1u) & 63u), 64);
             const int32_t e = j + 1u < 64u ? nx : (int32_t)rp_end;
+            hint = 0u;
             if (!(j < cnt_nodes && (int32_t)lane < e - b)) return 0xffffffffu;
-            const uint32_t id = (uint32_t)a.col[b + (int32_t)lane];
-            return a.hint_cur[b + (int32_t)lane] == a.stamp_cur ? id | 0x80000000u : id;
+            hint = a.hint_cur[b + (int32_t)lane];
+            return (uint32_t)a.col[b + (int32_t)lane];
         };
-        uint32_t cid_cur = load_ids(0u);
+        auto with_hint = [&](uint32_t id, uint32_t hint) -> uint32_t {
+            return (id != 0xffffffffu && hint == a.stamp_cur) ? id | 0x80000000u : id;
+        };
+        uint32_t h_cur = 0u;
+        uint32_t cid_cur = load_ids(0u, h_cur);
+        cid_cur = with_hint(cid_cur, h_cur);
         for (uint32_t jn = 0; jn < cnt_nodes; jn++) {
             const uint64_t v = c0 + jn;
             const int32_t beg = __shfl((int)rp, (int)jn, 64);
             const int32_t nx = __shfl((int)rp, (int)((jn + 1u) & 63u), 64);
             const int32_t end = jn + 1u < 64u ? nx : (int32_t)rp_end;
-            const uint32_t cid_next = load_ids(jn + 1u);
-            // ---- gather: peers' whole slots (both lines) -> accumulator ----
-            for (int32_t cb = beg; cb < end; cb += 64) {
-                const int32_t np = min(64, end - cb);
-                uint32_t cid = cid_cur;
-                if (cb != beg) {  // peers beyond the first 64 (rare): loaded here
-                    cid = 0xffffffffu;
-                    if ((int32_t)lane < np) {
-                        cid = (uint32_t)a.col[cb + (int32_t)lane];
-                        if (a.hint_cur[cb + (int32_t)lane] == a.stamp_cur) cid |= 0x80000000u;
+            // ---- gather: peers' slots -> accumulator, in batches of 8 kYoungQ peers ----
+            // (the first batch is straight-line code: its loads go out before the next node's id
+            // prefetch, and no loop header makes the wave wait for that prefetch)
+            ulonglong2 q[kYoungQ], q2[kYoungQ];
+            auto issue = [&](uint32_t cid, int32_t pb) {
+#pragma unroll
+                for (int k = 0; k < kYoungQ; k++) {
+                    const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
+                    const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64);
+                    q[k] = make_ulonglong2(~0ull, ~0ull);  // tombstones: nothing to scatter
+                    q2[k] = make_ulonglong2(~0ull, ~0ull);
+                    if (p < 64u && u != 0xffffffffu) {
+                        const uint16_t* sl = a.slot_cur + (uint64_t)(u & 0x7fffffffu) * kSlotU16 + (lane & 7u) * 8u;
+                        q[k] = *reinterpret_cast<const ulonglong2*>(sl);
+                        if (u & 0x80000000u) q2[k] = *reinterpret_cast<const ulonglong2*>(sl + 64u);
                     }
                 }
-                t_col += (uint32_t)np;
-                unsigned long long ovf = 0ull;  // bit p: peer cb+p
-                for (int32_t pb = 0; pb < np; pb += 8 * kYoungQ) {
-                    ulonglong2 q[kYoungQ], q2[kYoungQ];
-                    uint32_t missk = 0u;  // bit k: group k's peer has a second line nobody announced
+            };
+            // bit p of ovf: peer p of the 64-peer chunk overflowed (its dense rows are read)
+            auto consume = [&](uint32_t cid, int32_t pb, int32_t np, unsigned long long& ovf) {
+                uint32_t missk = 0u;  // bit k: group k's peer has a second line nobody announced
 #pragma unroll
-                    for (int k = 0; k < kYoungQ; k++) {
-                        const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
-                        const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64);
-                        q[k] = make_ulonglong2(~0ull, ~0ull);  // tombstones: nothing to scatter
-                        q2[k] = make_ulonglong2(~0ull, ~0ull);
-                        if (p < 64u && u != 0xffffffffu) {
-                            const uint16_t* sl = a.slot_cur + (uint64_t)(u & 0x7fffffffu) * kSlotU16 + (lane & 7u) * 8u;
-                            q[k] = *reinterpret_cast<const ulonglong2*>(sl);
-                            if (u & 0x80000000u) q2[k] = *reinterpret_cast<const ulonglong2*>(sl + 64u);
-                        }
+                for (int k = 0; k < kYoungQ; k++) {
+                    if (pb + k * 8 >= np) break;  // (uniform) no peer in this group of 8
+                    const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
+                    const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64);
+                    const bool valid = p < 64u && u != 0xffffffffu;
+                    const bool hinted = valid && (u & 0x80000000u);
+                    const uint32_t hdr = valid ? (uint32_t)__shfl((int)(q[k].x & 0xffffull), (int)(lane & ~7u), 64) : 0u;
+                    t_sl += wave_count(valid && (lane & 7u) == 0u) + wave_count(hinted && (lane & 7u) == 0u);
+                    // an overflowed slot's entries are a subset of its dense rows (read below)
+                    scatter8(q[k], (lane & 7u) == 0u);
+                    const bool two = hdr != kSlotOverflow && hdr > 63u;
+                    if (__ballot(two || hinted)) {  // (uniform) some second line in this group
+                        if (two && !hinted) missk |= 1u << k;  // fetched after the batch
+                        if (!two) q2[k] = make_ulonglong2(~0ull, ~0ull);  // stale hint
+                        scatter8(q2[k], false);
                     }
+                    const unsigned long long mo = __ballot((lane & 7u) == 0u && valid && hdr == kSlotOverflow);
+                    if (mo) {
 #pragma unroll
-                    for (int k = 0; k < kYoungQ; k++) {
-                        if (pb + k * 8 >= np) break;  // (uniform) no peer in this group of 8
-                        const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
-                        const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64);
-                        const bool valid = p < 64u && u != 0xffffffffu;
-                        const bool hinted = valid && (u & 0x80000000u);
-                        const uint32_t hdr = valid ? (uint32_t)__shfl((int)(q[k].x & 0xffffull), (int)(lane & ~7u), 64) : 0u;
-                        t_sl += wave_count(valid && (lane & 7u) == 0u) + wave_count(hinted && (lane & 7u) == 0u);
-                        // an overflowed slot's entries are a subset of its dense rows (read below)
-                        scatter8(q[k], (lane & 7u) == 0u);
-                        const bool two = hdr != kSlotOverflow && hdr > 63u;
-                        if (__ballot(two || hinted)) {  // (uniform) some second line in this group
-                            if (two && !hinted) missk |= 1u << k;  // fetched after the batch
-                            if (!two) q2[k] = make_ulonglong2(~0ull, ~0ull);  // stale hint
-                            scatter8(q2[k], false);
-                        }
-                        const unsigned long long mo = __ballot((lane & 7u) == 0u && valid && hdr == kSlotOverflow);
-                        if (mo) {
-#pragma unroll
-                            for (int g = 0; g < 8; g++)
-                                if ((mo >> (8 * g)) & 1ull) ovf |= 1ull << (((uint32_t)pb + (uint32_t)k * 8u + (uint32_t)g) & 63u);
-                        }
-                    }
-                    if (__ballot(missk != 0u)) {  // (uniform, rare) unannounced second lines
-                        for (int k = 0; k < kYoungQ; k++) {
-                            const bool miss = (missk >> k) & 1u;
-                            if (!__ballot(miss)) continue;
-                            const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
-                            const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64) & 0x7fffffffu;
-                            ulonglong2 x = make_ulonglong2(~0ull, ~0ull);
-                            if (miss) x = *reinterpret_cast<const ulonglong2*>(a.slot_cur + (uint64_t)u * kSlotU16 + 64u + (lane & 7u) * 8u);
-                            t_miss += wave_count(miss && (lane & 7u) == 0u);
-                            scatter8(x, false);
-                        }
+                        for (int g = 0; g < 8; g++)
+                            if ((mo >> (8 * g)) & 1ull) ovf |= 1ull << (((uint32_t)pb + (uint32_t)k * 8u + (uint32_t)g) & 63u);
                     }
                 }
+                if (__ballot(missk != 0u)) {  // (uniform, rare) unannounced second lines
+                    for (int k = 0; k < kYoungQ; k++) {
+                        const bool miss = (missk >> k) & 1u;
+                        if (!__ballot(miss)) continue;
+                        const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
+                        const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64) & 0x7fffffffu;
+                        ulonglong2 x = make_ulonglong2(~0ull, ~0ull);
+                        if (miss) x = *reinterpret_cast<const ulonglong2*>(a.slot_cur + (uint64_t)u * kSlotU16 + 64u + (lane & 7u) * 8u);
+                        t_miss += wave_count(miss && (lane & 7u) == 0u);
+                        scatter8(x, false);
+                    }
+                }
+            };
+            auto fallback = [&](uint32_t cid, unsigned long long ovf) {
                 while (ovf) {  // overflowed peers: their dense rows of every read-sparse tile
                     const int p = __builtin_ctzll(ovf);
                     ovf &= ovf - 1ull;
@@ -253,6 +253,32 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
                     }
                     t_fb += a.nr;
                 }
+            };
+            const int32_t np0 = min(64, end - beg);
+            t_col += (uint32_t)max(0, end - beg);
+            unsigned long long ovf = 0ull;
+            issue(cid_cur, 0);
+            uint32_t h_next = 0u;
+            const uint32_t cid_next = load_ids(jn + 1u, h_next);  // the next node's peers
+            consume(cid_cur, 0, np0, ovf);
+            for (int32_t pb = 8 * kYoungQ; pb < np0; pb += 8 * kYoungQ) {  // degree > 8 kYoungQ
+                issue(cid_cur, pb);
+                consume(cid_cur, pb, np0, ovf);
+            }
+            fallback(cid_cur, ovf);
+            for (int32_t cb = beg + 64; cb < end; cb += 64) {  // peers beyond the first 64 (rare)
+                const int32_t np = min(64, end - cb);
+                uint32_t cid = 0xffffffffu;
+                if ((int32_t)lane < np) {
+                    cid = (uint32_t)a.col[cb + (int32_t)lane];
+                    if (a.hint_cur[cb + (int32_t)lane] == a.stamp_cur) cid |= 0x80000000u;
+                }
+                unsigned long long ovf2 = 0ull;
+                for (int32_t pb = 0; pb < np; pb += 8 * kYoungQ) {
+                    issue(cid, pb);
+                    consume(cid, pb, np, ovf2);
+                }
+                fallback(cid, ovf2);
             }
             __builtin_amdgcn_wave_barrier();
             // ---- touched words -> list ----
@@ -302,7 +328,7 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
                 t_swr += wave_count(x != 0ull);
             }
             __builtin_amdgcn_wave_barrier();
-            cid_cur = cid_next;  // (arrived long ago: the wait here is before this node's stores)
+            cid_cur = with_hint(cid_next, h_next);  // (arrived long ago: the wait is before the stores)
             // ---- output: slot entries, or dense rows (overflowed / leaving the young set) ----
             const uint32_t total = (uint32_t)wave_sum((unsigned long long)cnt_sp);
             const bool overflow = total > a.cap;
