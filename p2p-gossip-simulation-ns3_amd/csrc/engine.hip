@@ -106,6 +106,7 @@ struct PullArgs {
     // 1: another kernel (k_pull_young) runs concurrently and shares the per-node outputs, so
     // counters are added and occupancy bits OR'ed atomically (nz_next zeroed beforehand)
     uint32_t shared_out = 0;
+    uint32_t keep_lds = 0;  // some word of the launch has WF_KEEP: masks staged in LDS (k_pull)
 };
 
 // Phase-ordered update of id groups inside one word (rare: only words holding groups).
@@ -1340,6 +1341,7 @@ int gossip_engine::tick_step_a(int64_t t) {
     const size_t nsnap = batch ? snaps.size() : 0;
     bool smask_any = false;
     if (nsnap && hw) std::memset(h_smask[slot], 0, (size_t)nsnap * hw * 8);
+    bool keep_any = false;  // some word has a keep mask (k_pull stages them in LDS)
     for (uint32_t w = 0; w < hw; w++) {
         WordCtl c = ctl[w];
         if (batch) {
@@ -1376,6 +1378,7 @@ int gossip_engine::tick_step_a(int64_t t) {
         C[w] = c;
         WF[w] = (uint8_t)((c.clear ? WF_CLEAR : 0u) | (c.gmask ? WF_GROUP : 0u) |
                           (c.keep != ~0ull ? WF_KEEP : 0u) | (c.snap ? WF_SNAP : 0u));
+        keep_any |= c.keep != ~0ull;
     }
     for (uint32_t i = 0; i < ny; i++)  // k_pull leaves these words to k_pull_young
         if (YP->yt[i].flags)
@@ -1412,6 +1415,7 @@ int gossip_engine::tick_step_a(int64_t t) {
         a.n = v1; a.stride = stride; a.wbase = 0; a.wact = wact;
         a.v0 = v0;  // row partition: this engine's rows [v0, v1)
         a.noskip = (cfg.flags & GOSSIP_F_NOSKIP) ? 1u : 0u;
+        a.keep_lds = keep_any ? 1u : 0u;
         const uint64_t chunks = ((uint64_t)(v1 - v0) + 63) / 64;  // 64 nodes per wave step sequence
         // non-temporal rows iff the frontier the launch gathers from (n rows x wact live words)
         // exceeds kPullNtBytes
@@ -1444,7 +1448,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 if (wide)
                     k_pull_wide<<<grid, 256, pull_lds_bytes(c.wact), stream>>>(c);
                 else
-                    launch_pull(lpw, epn, nt_rows, grid, pull_lds_bytes(c.wact), stream, c);
+                    launch_pull(lpw, epn, nt_rows, grid, pull_lds_bytes(c.wact, c.keep_lds != 0), stream, c);
             }
         };
         hipEvent_t e0 = nullptr, e1 = nullptr, p0 = nullptr, p1 = nullptr;

@@ -83,8 +83,10 @@ __device__ __forceinline__ void store_row16(uint64_t* p, uint64_t x, uint64_t y)
     }
 }
 
-__host__ __device__ constexpr size_t pull_lds_bytes(uint32_t wact) {
-    return (size_t)wact * 16u + (((size_t)wact + 15u) & ~(size_t)15u);
+// + the keep masks of the launch's words when some word has WF_KEEP (the cut tick): read from
+// LDS, a flagged word's mask never makes the wave wait on a global load
+__host__ __device__ constexpr size_t pull_lds_bytes(uint32_t wact, bool keep = false) {
+    return (size_t)wact * 16u + (((size_t)wact + 15u) & ~(size_t)15u) + (keep ? (size_t)wact * 8u : 0u);
 }
 
 // Peer ids of the first GRP peers of item k's node (0xffffffff past the list).
@@ -118,12 +120,14 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     unsigned long long* s_lp = smem;             // live_prev of this launch's words
     unsigned long long* s_new = smem + a.wact;   // liveness of this tick (OR of new bits)
     uint8_t* s_wf = reinterpret_cast<uint8_t*>(smem + 2u * a.wact);
+    unsigned long long* s_keep = smem + 2u * a.wact + ((a.wact + 15u) & ~15u) / 8u;
     for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
         const uint8_t f = a.wflags[a.wbase + i];
         // a young word is k_pull_young's: dead here, no clear, no write
         s_lp[i] = (f & WF_YOUNG) ? 0ull : (a.live_prev && !a.noskip) ? a.live_prev[a.wbase + i] : ~0ull;
         s_new[i] = 0ull;
         s_wf[i] = (f & WF_YOUNG) ? (uint8_t)0 : f;
+        if (a.keep_lds) s_keep[i] = (f & WF_KEEP) ? a.ctl[a.wbase + i].keep : ~0ull;
     }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -160,6 +164,10 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             t_nz += wave_count(cid0 != 0xffffffffu);
         }
         uint32_t cnt = 0;
+        // the first item's loads have landed before the item loop: inside it, every load is
+        // then waited for by the item that issued it or the next (a loop header that merged a
+        // pending first-item load would make every item wait for its own prefetches)
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
         while (step < nsteps) {
             // ---- geometry of this item and the next two ----
             const uint32_t step1 = pass + 1u < npass ? step : step + 1u;
@@ -210,8 +218,8 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             if (f0 & WF_CLEAR) s2.x = 0ull;
             if (f1 & WF_CLEAR) s2.y = 0ull;
             uint64_t k0 = ~0ull, k1 = ~0ull;
-            if (act && (f0 & WF_KEEP)) k0 = a.ctl[w].keep;
-            if (act && (f1 & WF_KEEP)) k1 = a.ctl[w + 1].keep;
+            if (act && (f0 & WF_KEEP)) k0 = s_keep[w - a.wbase];
+            if (act && (f1 & WF_KEEP)) k1 = s_keep[w + 1 - a.wbase];
             // (incoming mode must consume every live pair's incoming word: no saturation skip)
             const bool need = act && !dead &&
                               (a.noskip || a.inc || ((lp0 & ~s2.x & k0) | (lp1 & ~s2.y & k1)) != 0ull);
@@ -250,16 +258,8 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                     // every F_cur bit lies inside live_prev, and seen / not-kept bits are
                     // masked out of `new`, so peers beyond covering these add nothing.
                     const uint64_t want0 = lp0 & ~s2.x & k0, want1 = lp1 & ~s2.y & k1;
-                    for (int32_t cb = beg; cb < end; cb += GRP) {
-                        uint32_t cid = cid0;
-                        unsigned long long nzw = nz0;
-                        const int rem = min(GRP, end - cb);
-                        if (cb != beg) {  // peers beyond the first GRP: loaded inline (rare)
-                            const int32_t jj = cb + (int32_t)gl;
-                            cid = (jj < end) ? (uint32_t)a.col[jj] : 0u;
-                            nzw = ((int)gl < rem) ? a.nz_cur[(uint64_t)cid * a.ntw + tw] : 0ull;
-                            t_nz += wave_count((int)gl < rem);
-                        }
+                    // one lane group's worth of peers (ids in `cid`, occupancy words in `nzw`)
+                    auto gchunk = [&](uint32_t cid, unsigned long long nzw, int rem) {
                         t_col += wave_count((int)gl < rem);
                         // the <= 8 occupancy bits of this pass's tiles, tested per lane by tile
                         const uint32_t nzp = (uint32_t)(nzw >> ((((w - 2u * wl) >> 4)) & 63u)) & 0xffu;
@@ -293,6 +293,18 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                                 acc1 |= q[t].y;
                             }
                         }
+                    };
+                    // the first lane group of peers is straight-line code (its ids and occupancy
+                    // came with the previous item), so no loop header makes the wave wait for
+                    // the loads this item just issued for the next ones
+                    gchunk(cid0, nz0, min(GRP, end - beg));
+                    for (int32_t cb = beg + GRP; cb < end; cb += GRP) {  // more peers (rare)
+                        const int rem = min(GRP, end - cb);
+                        const int32_t jj = cb + (int32_t)gl;
+                        const uint32_t cid = (jj < end) ? (uint32_t)a.col[jj] : 0u;
+                        const unsigned long long nzw = ((int)gl < rem) ? a.nz_cur[(uint64_t)cid * a.ntw + tw] : 0ull;
+                        t_nz += wave_count((int)gl < rem);
+                        gchunk(cid, nzw, rem);
                     }
                 } else {
                     // edge-lane el walks peers beg+el, beg+el+EPN, ...; 8 in flight
