@@ -241,9 +241,13 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *                                                                          [GOSSIP_YOUNG_AGE]
  *   "young_cap"        slot entries per node before it falls back to dense rows (1..127)
  *                                                                          [GOSSIP_YOUNG_CAP]
+ *   "pull_gate"        1: k_pull skips the own-seen loads of tiles no peer holds a row of (the
+ *                      default), 0: reads every live pair                     [GOSSIP_PULL_GATE]
+ *   "young_grid"       k_pull_young blocks, 0 = the pull grid                [GOSSIP_YOUNG_GRID]
  *   "young_overlap"    0: k_pull_young after k_pull on the engine stream; 1: the two run
  *                      concurrently on two streams, k_pull_young launched first (default);
- *                      2: concurrently, k_pull launched first            [GOSSIP_YOUNG_OVERLAP]
+ *                      2: concurrently, k_pull launched first; 3 / 4: as 1 with the second
+ *                      stream at the lowest / highest priority          [GOSSIP_YOUNG_OVERLAP]
  *   "mem_limit"        bytes of device memory the engine may hold, 0 = what the device has
  *                      free; a window that outgrows it fails with GOSSIP_ECAPACITY / ENOMEM
  *                      (callers then split the shares into more shards)   [GOSSIP_MEM_LIMIT] */

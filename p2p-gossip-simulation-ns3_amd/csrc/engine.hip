@@ -107,6 +107,7 @@ struct PullArgs {
     // counters are added and occupancy bits OR'ed atomically (nz_next zeroed beforehand)
     uint32_t shared_out = 0;
     uint32_t keep_lds = 0;  // some word of the launch has WF_KEEP: masks staged in LDS (k_pull)
+    uint32_t gate_seen = 1;  // k_pull<LPW,1>: skip the own-seen loads of tiles no peer occupies
 };
 
 // Phase-ordered update of id groups inside one word (rare: only words holding groups).
@@ -569,6 +570,7 @@ struct gossip_engine {
     int64_t opt_young_cap = 127;      // slot entries per node before it overflows to dense rows
     int64_t opt_young_overlap = 1;    // k_pull_young beside k_pull on a second stream (1-4) or after (0)
     int64_t opt_young_grid = 0;       // k_pull_young blocks, 0 = the pull grid
+    int64_t opt_pull_gate = 1;        // k_pull: occupancy-gated own-seen loads
     hipStream_t ystream = nullptr;    // the second stream (created on first use)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers_phase;  // pull phase (both kernels)
@@ -1416,6 +1418,7 @@ int gossip_engine::tick_step_a(int64_t t) {
         a.v0 = v0;  // row partition: this engine's rows [v0, v1)
         a.noskip = (cfg.flags & GOSSIP_F_NOSKIP) ? 1u : 0u;
         a.keep_lds = keep_any ? 1u : 0u;
+        a.gate_seen = opt_pull_gate ? 1u : 0u;
         const uint64_t chunks = ((uint64_t)(v1 - v0) + 63) / 64;  // 64 nodes per wave step sequence
         // non-temporal rows iff the frontier the launch gathers from (n rows x wact live words)
         // exceeds kPullNtBytes
@@ -1944,6 +1947,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_young_cap = env_option("GOSSIP_YOUNG_CAP", 127);
         e->opt_young_overlap = env_option("GOSSIP_YOUNG_OVERLAP", 1);
         e->opt_young_grid = env_option("GOSSIP_YOUNG_GRID", 0);
+        e->opt_pull_gate = env_option("GOSSIP_PULL_GATE", 1);
         e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
         e->dense = cfg->mode == GOSSIP_MODE_DENSE;
@@ -2205,6 +2209,9 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     } else if (k == "young_overlap") {
         if (value < 0 || value > 4) return set_error(GOSSIP_EINVAL, "young_overlap: 0 .. 4");
         e->opt_young_overlap = value;
+    } else if (k == "pull_gate") {
+        if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "pull_gate: 0 or 1");
+        e->opt_pull_gate = value;
     } else if (k == "young_grid") {
         if (value < 0 || value > (1 << 20)) return set_error(GOSSIP_EINVAL, "young_grid: 0 .. 2^20 blocks");
         e->opt_young_grid = value;

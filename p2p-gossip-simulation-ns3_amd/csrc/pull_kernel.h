@@ -164,6 +164,14 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             t_nz += wave_count(cid0 != 0xffffffffu);
         }
         uint32_t cnt = 0;
+        // Occupancy gate of the own-seen loads: nzor = OR over the node's peers of their
+        // occupancy word (recomputed when the word changes); a tile no peer holds a row of
+        // receives nothing, so its seen pair is not read (s2 gated: no gather, no write).
+        // Only for nodes whose peers fit in one lane group, and only for the next item of the
+        // same node and occupancy word (whose nz word is already in registers).
+        unsigned long long nzor = 0ull;
+        bool nz_new = true, s2c_gated = false;
+        const bool gate = gather && !a.noskip && a.gate_seen;
         // the first item's loads have landed before the item loop: inside it, every load is
         // then waited for by the item that issued it or the next (a loop header that merged a
         // pending first-item load would make every item wait for its own prefetches)
@@ -179,12 +187,28 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             const bool act = c0 + idx < n && w < a.wbase + a.wact;
             // ---- stage loads: own seen pair of item k+1, ids of k+2, occupancy of k+1 ----
             ulonglong2 s2n = make_ulonglong2(0ull, 0ull);
+            bool s2n_gated = false;
+            if (gate && nz_new) {  // (uniform) this item starts a new occupancy word
+                unsigned long long x = nz0;
+#pragma unroll
+                for (int off = GRP / 2; off > 0; off >>= 1) x |= __shfl_xor(x, off, GRP);
+                nzor = x;
+                nz_new = false;
+            }
             if (step1 < nsteps) {
                 // (a dead pair's seen words are never needed: only cleared, never merged)
                 const uint64_t v1 = c0 + step1 * NPW + slot;
                 const uint32_t lw1 = pass1 * 2u * LPW + 2u * wl;
-                if (v1 < n && lw1 < a.wact && (s_lp[lw1] | s_lp[lw1 + 1u]) != 0ull)
-                    s2n = load_row16<NT>(a.seen + v1 * stride + a.wbase + lw1);
+                if (v1 < n && lw1 < a.wact && (s_lp[lw1] | s_lp[lw1 + 1u]) != 0ull) {
+                    // same node and occupancy word as this item, peers in one lane group
+                    const uint32_t ix = step * NPW + slot;
+                    const int32_t b0 = __shfl((int)rp, (int)ix, 64);
+                    const int32_t e0 = ix + 1u < 64u ? __shfl((int)rp, (int)((ix + 1u) & 63u), 64) : (int32_t)rp_end;
+                    s2n_gated = gate && step1 == step &&
+                                ((a.wbase + lw1) >> 10) == ((a.wbase + pass * 2u * LPW) >> 10) && e0 - b0 <= GRP &&
+                                !((nzor >> (((a.wbase + lw1) >> 4) & 63u)) & 1ull);
+                    if (!s2n_gated) s2n = load_row16<NT>(a.seen + v1 * stride + a.wbase + lw1);
+                }
             }
             uint32_t cid2 = 0xffffffffu;
             unsigned long long nz1 = 0ull;
@@ -221,7 +245,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             if (act && (f0 & WF_KEEP)) k0 = s_keep[w - a.wbase];
             if (act && (f1 & WF_KEEP)) k1 = s_keep[w + 1 - a.wbase];
             // (incoming mode must consume every live pair's incoming word: no saturation skip)
-            const bool need = act && !dead &&
+            const bool need = act && !dead && !s2c_gated &&
                               (a.noskip || a.inc || ((lp0 & ~s2.x & k0) | (lp1 & ~s2.y & k1)) != 0ull);
             // Columns are allocated in 16-word tiles (one 128-B line per row, engine.hip), so the
             // read decision is made per tile: the 8 word-lanes of a tile load together and every
@@ -366,7 +390,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             const bool swr = own && (dead ? ((f0 | f1) & WF_CLEAR) != 0u
                                           : ((n0 | n1) != 0ull || ((f0 | f1) & WF_CLEAR) != 0u));
             t_fwr += wave_count(own && ta);
-            t_srd += wave_count(own && !dead);
+            t_srd += wave_count(own && !dead && !s2c_gated);
             t_swr += wave_count(swr);
             if (own) {
                 uint64_t* sp = a.seen + (uint64_t)v * stride + w;
@@ -423,8 +447,10 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             }
             // ---- advance the pipeline ----
             s2c = s2n;
+            s2c_gated = s2n_gated;
             cid0 = cid1;
             cid1 = cid2;
+            nz_new = step1 != step || ((a.wbase + pass1 * 2u * LPW) >> 10) != ((a.wbase + pass * 2u * LPW) >> 10);
             nz0 = nz1;
             step = step1;
             pass = pass1;

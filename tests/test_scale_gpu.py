@@ -154,6 +154,7 @@ def test_c4_sample_matches_oracle_a(gossip, oracle, c4):
         ("nt rows, 16384-block grid (the C4 production kernel)", (("pull_nt", 1), ("pull_grid", 16384))),
         ("nt rows, 3-block grid", (("pull_nt", 1), ("pull_grid", 3))),
         ("64 word-lanes", (("pull_lpw", 64),)),
+        ("every live seen pair read (no occupancy gate)", (("pull_gate", 0),)),
     ]
     for name, opts in variants:
         st, c = _run(gossip, topo, ev, W.T0_NS, t_cut, options=opts, max_words=16)
