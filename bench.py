@@ -63,7 +63,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(name, line):
+def pmc_traffic(name, line, variant):
     """HBM bytes per pull launch from the committed rocprofv3 PMC pass of this workload
     (profiles/pmc_<workload>.json, written by tools/pmc_traffic.py), only when that pass ran the
     same configuration as this line; otherwise (None, reason)."""
@@ -78,9 +78,9 @@ def pmc_traffic(name, line):
     except Exception as e:  # a malformed file is reported, not fatal
         return None, f"unreadable PMC file: {e}"
     cfg = d.get("config") or {}
-    want = {"workload": name, "warmup": line["warmup"], "steps": line["steps"],
+    want = {"workload": name.split("_")[0], "warmup": line["warmup"], "steps": line["steps"],
             "live_words_per_node": line["config"]["live_words_per_node"],
-            "pull_variant": line["roofline"]["pull_variant"]}
+            "pull_variant": variant}
     diff = {k: (cfg.get(k), v) for k, v in want.items() if cfg.get(k) != v}
     if diff:
         return None, f"PMC pass config differs from this line: {diff}"
@@ -320,46 +320,44 @@ def main():
                 "device_gib": acc["dev_bytes"] / 2**30,
                 "parallelism": f"share-shard x{shards} over {max(world, 1)} rank(s)",
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
-                "kernel": "k_pull",
-                "pull_variant": {"nt_rows": acc["nt"], "grid": acc["grid"],
-                                 "young_overlap": YOUNG_OVERLAP if acc["young_launches"] else None},
-                "bytes_per_launch": bytes_per_launch,
-                "bytes_note": "algorithmic bytes of the occupancy-skipping pull: the peer-row, "
-                              "peer-id, occupancy, own-row and counter bytes it must move",
-                "dense_formula_bytes_per_launch": dense_bytes_per_launch,
-                "dense_formula_frac": ((dense_bytes_per_launch / (avg_ms * 1e6)) / HBM_PEAK_GBS) if avg_ms > 0 else None,
-                "dense_formula_note": "SURVEY 8(d) B = 8(n+1)+4nnz+8Wq*nnz+24Wq*n+16n assumes every "
-                                      "peer-row word is read; the kernel skips dead, saturated and "
-                                      "unoccupied rows, so this ratio can exceed 1 and is not a "
-                                      "roofline fraction",
-                "avg_launch_ms": avg_ms,
-                "launches": launches,
-                "bytes_breakdown_per_launch": {
-                    "peer_rows": per_launch(16 * acc["pe"]),
-                    "peer_ids": per_launch(4 * acc["col"]),
-                    "peer_occupancy": per_launch(8 * acc["nz"]),
-                    "own_seen_read": per_launch(16 * acc["srd"]),
-                    "own_seen_write": per_launch(16 * acc["swr"]),
-                    "frontier_write": per_launch(16 * acc["fwr"]),
-                    "per_node_rowptr_counters_occupancy": per_launch(
-                        acc["moved"] - 16 * acc["pe"] - 4 * acc["col"] - 8 * acc["nz"] -
-                        16 * (acc["srd"] + acc["swr"] + acc["fwr"])),
-                },
-                "pull_fraction_of_step": (((acc["phase_ms"] or (pull_ms_max + acc["young_ms"])) / (elapsed * 1e3))
-                                          if elapsed > 0 else None),
+            "roofline": None,
+        }
+        k_pull = {
+            "kernel": "k_pull",
+            "avg_launch_ms": avg_ms,
+            "launches": launches,
+            "bytes_per_launch": bytes_per_launch,
+            "achieved": achieved,
+            "frac": achieved / HBM_PEAK_GBS,
+            "bytes_note": "algorithmic bytes of the occupancy-skipping pull: the peer-row, peer-id, "
+                          "occupancy, own-row and counter bytes it must move",
+            "dense_formula_bytes_per_launch": dense_bytes_per_launch,
+            "dense_formula_frac": ((dense_bytes_per_launch / (avg_ms * 1e6)) / HBM_PEAK_GBS) if avg_ms > 0 else None,
+            "dense_formula_note": "SURVEY 8(d) B = 8(n+1)+4nnz+8Wq*nnz+24Wq*n+16n assumes every "
+                                  "peer-row word is read; the kernel skips dead, saturated and "
+                                  "unoccupied rows, so this ratio can exceed 1 and is not a "
+                                  "roofline fraction",
+            "bytes_breakdown_per_launch": {
+                "peer_rows": per_launch(16 * acc["pe"]),
+                "peer_ids": per_launch(4 * acc["col"]),
+                "peer_occupancy": per_launch(8 * acc["nz"]),
+                "own_seen_read": per_launch(16 * acc["srd"]),
+                "own_seen_write": per_launch(16 * acc["swr"]),
+                "frontier_write": per_launch(16 * acc["fwr"]),
+                "per_node_rowptr_counters_occupancy": per_launch(
+                    acc["moved"] - 16 * acc["pe"] - 4 * acc["col"] - 8 * acc["nz"] -
+                    16 * (acc["srd"] + acc["swr"] + acc["fwr"])),
             },
         }
+        variant = {"nt_rows": acc["nt"], "grid": acc["grid"],
+                   "young_overlap": YOUNG_OVERLAP if acc["young_launches"] else None}
+        t_pull, why_pull = pmc_traffic(wl["name"], out, variant)
+        k_pull["traffic"] = t_pull
+        young = None
         if acc["young_launches"]:
             yl = acc["young_launches"]
             y_ms = acc["young_ms"] / yl
-            out["roofline"]["young_tiles"] = {
+            young = {
                 "kernel": "k_pull_young",
                 "avg_launch_ms": y_ms,
                 "launches": yl,
@@ -379,20 +377,42 @@ def main():
                     "unhinted_second_lines_read": 128 * acc.get("young_line2_misses", 0) / yl,
                 },
             }
-            # wall time of the phase (HIP events around both kernels on the engine stream; they
-            # run concurrently on two streams when young_overlap is on)
-            tot_ms = (acc["phase_ms"] / max(launches, 1)) if acc["phase_ms"] else \
+            t_young, why_young = pmc_traffic(wl["name"] + "_young", out, variant)
+            young["traffic"] = t_young
+        if young is None:
+            roof = dict(k_pull)
+            roof.update({"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "pull_variant": variant})
+            if why_pull:
+                roof["traffic_note"] = why_pull
+        else:
+            # The pull phase: k_pull and k_pull_young, concurrent on two streams (young_overlap),
+            # timed as one unit by HIP events around both on the engine stream.  Its bytes are
+            # the two kernels' algorithmic bytes, its traffic the sum of their PMC passes.
+            ph_ms = (acc["phase_ms"] / max(launches, 1)) if acc["phase_ms"] else \
                 avg_ms + acc["young_ms"] / max(launches, 1)
-            tot_b = bytes_per_launch + acc["young_bytes"] / max(launches, 1)
-            out["roofline"]["pull_phase"] = {
-                "kernels": "k_pull + k_pull_young" + (" (concurrent, two streams)" if YOUNG_OVERLAP else ""),
-                "ms_per_tick": tot_ms, "bytes_per_tick": tot_b,
-                "achieved": tot_b / (tot_ms * 1e6) if tot_ms > 0 else None,
-                "frac": (tot_b / (tot_ms * 1e6)) / HBM_PEAK_GBS if tot_ms > 0 else None}
-        traffic, why = pmc_traffic(wl["name"], out)
-        out["roofline"]["traffic"] = traffic
-        if why:
-            out["roofline"]["traffic_note"] = why
+            ph_b = bytes_per_launch + young["bytes_per_launch"]
+            ph_ach = ph_b / (ph_ms * 1e6) if ph_ms > 0 else 0.0
+            traffic = (t_pull + t_young) if (t_pull is not None and t_young is not None) else None
+            roof = {
+                "bound": "hbm",
+                "achieved": ph_ach,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": ph_ach / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "pull phase: k_pull + k_pull_young" +
+                          (" (concurrent, two streams)" if YOUNG_OVERLAP else " (in sequence)"),
+                "avg_launch_ms": ph_ms,
+                "launches": launches,
+                "bytes_per_launch": ph_b,
+                "pull_variant": variant,
+                "kernels": {"k_pull": k_pull, "k_pull_young": young},
+            }
+            why = "; ".join(w for w in (why_pull, why_young) if w)
+            if why:
+                roof["traffic_note"] = why
+        roof["pull_fraction_of_step"] = ((roof["avg_launch_ms"] * launches / 1e3) / elapsed) if elapsed > 0 else None
+        out["roofline"] = roof
         if n_gpus == 1 and world == 1 and not args.no_cpu_baseline:
             try:
                 win = ev[ev["ns"] >= SLICE_NS]

@@ -70,8 +70,11 @@ def main():
                          "warmup": line["warmup"], "steps": line["steps"],
                          "live_words_per_node": line["config"]["live_words_per_node"],
                          "pull_variant": line["roofline"]["pull_variant"]}
-        out["algorithmic_bytes_per_launch"] = line["roofline"]["bytes_per_launch"]
-        out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / line["roofline"]["bytes_per_launch"]
+        roof = line["roofline"]
+        kern = roof.get("kernels") or {}
+        src = kern.get("k_pull_young" if "young" in a.kernel else "k_pull") or roof
+        out["algorithmic_bytes_per_launch"] = src["bytes_per_launch"]
+        out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / src["bytes_per_launch"]
     s = json.dumps(out, indent=1)
     if a.out:
         with open(a.out, "w") as fh:

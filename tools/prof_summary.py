@@ -22,6 +22,9 @@ def main():
                     help="engine passes in the run (share shards per GPU): the timed "
                          "dispatches are the last K of each pass")
     ap.add_argument("--kernel", default="k_pull<", help="substring of the kernel name")
+    ap.add_argument("--phase-with", help="substring of a second kernel launched beside --kernel "
+                                          "every tick (on another stream): also report the "
+                                          "timed ticks' phase = first start to last end of both")
     ap.add_argument("--out")
     a = ap.parse_args()
     stats = list(csv.DictReader(open(os.path.join(a.prof_dir, f"{a.run}_kernel_stats.csv"))))
@@ -45,6 +48,18 @@ def main():
         "lds_bytes": int(pulls[-1]["LDS_Block_Size"]) if pulls else None,
         "grid": int(pulls[-1]["Grid_Size_X"]) if pulls else None,
     }
+    if a.phase_with:
+        other = [r for r in trace if a.phase_with in r["Kernel_Name"]]
+        x = [r for q in range(P) for r in pulls[q * per:(q + 1) * per][-a.timed:]]
+        # the partner of a timed dispatch: the other kernel's dispatch that started closest to it
+        y = [min(other, key=lambda o: abs(int(o["Start_Timestamp"]) - int(p["Start_Timestamp"]))) for p in x]
+        ph = [(max(int(p["End_Timestamp"]), int(o["End_Timestamp"])) -
+               min(int(p["Start_Timestamp"]), int(o["Start_Timestamp"]))) / 1e6 for p, o in zip(x, y)]
+        yd = [(int(o["End_Timestamp"]) - int(o["Start_Timestamp"])) / 1e6 for o in y]
+        out["phase_with"] = a.phase_with
+        out["phase_ticks"] = len(ph)
+        out["phase_avg_ms"] = sum(ph) / max(len(ph), 1)
+        out["phase_with_avg_ms"] = sum(yd) / max(len(yd), 1)
     s = json.dumps(out, indent=1)
     if a.out:
         with open(a.out, "w") as f:
