@@ -244,6 +244,8 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *   "pull_gate"        1: k_pull skips the own-seen loads of tiles no peer holds a row of (the
  *                      default), 0: reads every live pair                     [GOSSIP_PULL_GATE]
  *   "young_grid"       k_pull_young blocks, 0 = the pull grid                [GOSSIP_YOUNG_GRID]
+ *   "young_waves"      k_pull_young register budget in waves per SIMD: 4 (no spills), 5, 6
+ *                                                                         [GOSSIP_YOUNG_WAVES]
  *   "young_overlap"    0: k_pull_young after k_pull on the engine stream; 1: the two run
  *                      concurrently on two streams, k_pull_young launched first (default);
  *                      2: concurrently, k_pull launched first; 3 / 4: as 1 with the second

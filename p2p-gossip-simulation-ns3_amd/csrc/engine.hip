@@ -571,6 +571,7 @@ struct gossip_engine {
     int64_t opt_young_overlap = 1;    // k_pull_young beside k_pull on a second stream (1-4) or after (0)
     int64_t opt_young_grid = 0;       // k_pull_young blocks, 0 = the pull grid
     int64_t opt_pull_gate = 1;        // k_pull: occupancy-gated own-seen loads
+    int64_t opt_young_waves = 4;      // k_pull_young register budget: waves per SIMD (4, 5, 6)
     hipStream_t ystream = nullptr;    // the second stream (created on first use)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers_phase;  // pull phase (both kernels)
@@ -1511,7 +1512,13 @@ int gossip_engine::tick_step_a(int64_t t) {
                 y1 = get_event();
                 HIP_TRY(hipEventRecord(y0, ys));
             }
-            k_pull_young<<<yg, 256, young_lds_bytes(ny, ny_read), ys>>>(y);
+            const size_t ylds = young_lds_bytes(ny, ny_read);
+            if (opt_young_waves == 6)
+                k_pull_young<6><<<yg, 256, ylds, ys>>>(y);
+            else if (opt_young_waves == 5)
+                k_pull_young<5><<<yg, 256, ylds, ys>>>(y);
+            else
+                k_pull_young<4><<<yg, 256, ylds, ys>>>(y);
             HIP_TRY(hipGetLastError());
             if (cfg.flags & GOSSIP_F_TIMING) {
                 HIP_TRY(hipEventRecord(y1, ys));
@@ -1948,6 +1955,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_young_overlap = env_option("GOSSIP_YOUNG_OVERLAP", 1);
         e->opt_young_grid = env_option("GOSSIP_YOUNG_GRID", 0);
         e->opt_pull_gate = env_option("GOSSIP_PULL_GATE", 1);
+        e->opt_young_waves = env_option("GOSSIP_YOUNG_WAVES", 4);
         e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
         e->dense = cfg->mode == GOSSIP_MODE_DENSE;
@@ -2212,6 +2220,9 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     } else if (k == "pull_gate") {
         if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "pull_gate: 0 or 1");
         e->opt_pull_gate = value;
+    } else if (k == "young_waves") {
+        if (value < 4 || value > 6) return set_error(GOSSIP_EINVAL, "young_waves: 4, 5 or 6");
+        e->opt_young_waves = value;
     } else if (k == "young_grid") {
         if (value < 0 || value > (1 << 20)) return set_error(GOSSIP_EINVAL, "young_grid: 0 .. 2^20 blocks");
         e->opt_young_grid = value;

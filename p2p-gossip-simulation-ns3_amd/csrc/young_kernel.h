@@ -118,7 +118,9 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m, uint32_t l
     return (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-__global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
+// WAVES: waves per SIMD the register allocation must allow (young_waves option; 4 = no spills)
+template <int WAVES>
+__global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
     extern __shared__ unsigned long long smem[];
     const uint32_t nrw = a.nr * 16u;  // accumulated words
     const uint32_t accw = nrw + kYoungSpare;
