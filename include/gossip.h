@@ -205,10 +205,22 @@ int gossip_engine_group_run(gossip_engine** engines, uint32_t count, int64_t tic
  *   gossip_engine_exchange_export  copies the message to host memory (buf NULL: size only)
  *   gossip_engine_exchange_import  once per other rank, with that rank's message
  *   gossip_engine_tick_end         liveness, retirement, next tick
- * The messages are exactly those the RCCL backend broadcasts. */
+ * Pipelined form (what the RCCL backend does): the own rows are pulled in
+ * gossip_engine_exchange_chunks(e) row chunks (option "xchunks", default 4, equal on every rank;
+ * 512-row blocks), and chunk c's message can leave as soon as that chunk is computed, while the
+ * GPU computes chunk c + 1: per chunk c, export_chunk then import_chunk from every other rank
+ * (the rank's liveness words ride in its last chunk).  tick_begin only enqueues the tick's
+ * kernels; an export waits for its chunk on the engine's exchange stream.  The whole-rows
+ * export/import above are the same exchange in one message per rank (not to be mixed with the
+ * chunked calls inside one tick). */
 int gossip_engine_tick_begin(gossip_engine* e);
 int gossip_engine_exchange_export(gossip_engine* e, void* buf, uint64_t cap_bytes, uint64_t* bytes);
 int gossip_engine_exchange_import(gossip_engine* e, uint32_t rank, const void* buf, uint64_t bytes);
+int gossip_engine_exchange_chunks(const gossip_engine* e);
+int gossip_engine_exchange_export_chunk(gossip_engine* e, uint32_t chunk, void* buf, uint64_t cap_bytes,
+                                        uint64_t* bytes);
+int gossip_engine_exchange_import_chunk(gossip_engine* e, uint32_t rank, uint32_t chunk, const void* buf,
+                                        uint64_t bytes);
 int gossip_engine_tick_end(gossip_engine* e);
 
 /* NS-3 link timing: every hop of a share costs
@@ -252,7 +264,12 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *                      stream at the lowest / highest priority          [GOSSIP_YOUNG_OVERLAP]
  *   "mem_limit"        bytes of device memory the engine may hold, 0 = what the device has
  *                      free; a window that outgrows it fails with GOSSIP_ECAPACITY / ENOMEM
- *                      (callers then split the shares into more shards)   [GOSSIP_MEM_LIMIT] */
+ *                      (callers then split the shares into more shards)   [GOSSIP_MEM_LIMIT]
+ *   "late_age"         k_pull stops gathering a node's peer rows of a tile at least this many
+ *                      ticks old once they cover every bit it can still take (bottom-up early
+ *                      exit); 0 = off                                         [GOSSIP_LATE_AGE]
+ *   "xchunks"          row partition: row chunks per tick of the pipelined exchange, 1..16 (4);
+ *                      equal on every rank of a partition                    [GOSSIP_XCHUNKS] */
 int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value);
 /* The mode the engine runs (AUTO resolves at gossip_engine_set_graph). */
 int gossip_engine_mode(const gossip_engine* e);

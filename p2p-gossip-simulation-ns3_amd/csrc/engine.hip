@@ -572,6 +572,7 @@ struct gossip_engine {
     int64_t opt_young_grid = 0;       // k_pull_young blocks, 0 = the pull grid
     int64_t opt_pull_gate = 1;        // k_pull: occupancy-gated own-seen loads
     int64_t opt_young_waves = 4;      // k_pull_young register budget: waves per SIMD (4, 5, 6)
+    int64_t opt_late_age = 0;         // k_pull early exit for tiles >= this many ticks old (0: off)
     hipStream_t ystream = nullptr;    // the second stream (created on first use)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers_phase;  // pull phase (both kernels)
@@ -615,8 +616,8 @@ struct gossip_engine {
     int tick_step_b(int64_t t);  // exchange (RCCL) + liveness read-back + bookkeeping
     int exchange_rccl(int64_t t);
     // compressed row exchange (row partition): message buffers and traffic counters
-    int pack_rows(int64_t t);
-    int unpack_rows(int64_t t, uint32_t r, const uint64_t* msg, uint64_t words);
+    int pack_rows(int64_t t, uint32_t c, hipStream_t s);
+    int unpack_rows(int64_t t, uint32_t r, uint32_t c, const uint64_t* msg, uint64_t words, hipStream_t s);
     int ensure_dev(uint64_t*& p, uint64_t& cap, uint64_t words);
     uint64_t* d_msg = nullptr;       // this rank's packed message
     uint64_t msg_cap = 0, msg_words = 0;
@@ -630,6 +631,21 @@ struct gossip_engine {
     uint64_t sizes_cap = 0;
     uint64_t exchange_bytes_out = 0, exchange_bytes_in = 0;
     bool tick_open = false;          // host-staged stepping: tick_begin done, tick_end pending
+    // Pipelined exchange (option xchunks, row partition only): the own rows go through the pull
+    // and the births in `nchunks` row chunks on the engine stream, chunk c ending with
+    // ev_chunk[c]; chunk c's message is packed, sent and the other ranks' chunk c unpacked on
+    // xstream while the engine stream computes chunk c + 1.  Every rank uses the same chunk
+    // count (checked by the RCCL backend).  kWholeRows = one message of all own rows.
+    static constexpr uint32_t kMaxChunks = 16, kWholeRows = 0xffffffffu;
+    int64_t opt_xchunks = 4;
+    uint32_t nchunks = 1;            // chunks of the current tick
+    hipStream_t xstream = nullptr;
+    hipEvent_t ev_chunk[kMaxChunks] = {};
+    hipEvent_t ev_xdone = nullptr;
+    int64_t packed_tick = -1;        // host-staged export: message of (tick, chunk) already packed
+    uint32_t packed_chunk = 0;
+    void chunk_rows(uint32_t r, uint32_t c, uint64_t* lo, uint64_t* hi) const;
+    int ensure_xstream();
     int retire_from(int64_t known_tick, const unsigned long long* live);
     int alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t);
     int grow(uint32_t new_stride);
@@ -639,6 +655,7 @@ struct gossip_engine {
 };
 
 gossip_engine::~gossip_engine() {
+    if (xstream) hipStreamSynchronize(xstream);
     if (stream) hipStreamSynchronize(stream);
     for (auto& p : timers) {
         hipEventDestroy(p.first);
@@ -676,6 +693,10 @@ gossip_engine::~gossip_engine() {
     if (ev_fork) hipEventDestroy(ev_fork);
     if (ev_join) hipEventDestroy(ev_join);
     if (ystream) hipStreamDestroy(ystream);
+    for (auto ev : ev_chunk)
+        if (ev) hipEventDestroy(ev);
+    if (ev_xdone) hipEventDestroy(ev_xdone);
+    if (xstream) hipStreamDestroy(xstream);
     if (stream) hipStreamDestroy(stream);
 }
 
@@ -1333,6 +1354,27 @@ int gossip_engine::tick_step_a(int64_t t) {
     } else {
         for (uint32_t q = 0; q < nb; q++) B[q].widx = 0xffu;
     }
+    // 3c. row chunks of the pipelined exchange: births grouped by chunk (a node has at most one
+    //     birth per tick, so their order inside a launch is free)
+    nchunks = row_count > 1 ? (uint32_t)std::min<int64_t>(kMaxChunks, std::max<int64_t>(1, opt_xchunks)) : 1u;
+    uint32_t cb_off[kMaxChunks + 1] = {};
+    cb_off[1] = nb;
+    if (nchunks > 1) {
+        uint64_t clo[kMaxChunks + 1];
+        for (uint32_t c = 0; c < nchunks; c++) chunk_rows(row_rank, c, &clo[c], &clo[c + 1]);
+        auto chunk_of = [&](uint32_t v) {
+            uint32_t c = 0;
+            while (c + 1 < nchunks && v >= clo[c + 1]) c++;
+            return c;
+        };
+        uint32_t cnt[kMaxChunks] = {};
+        for (uint32_t q = 0; q < nb; q++) cnt[chunk_of(B[q].node)]++;
+        for (uint32_t c = 0; c < nchunks; c++) cb_off[c + 1] = cb_off[c] + cnt[c];
+        std::vector<Birth> tmp(B, B + nb);
+        uint32_t at[kMaxChunks];
+        std::copy(cb_off, cb_off + nchunks, at);
+        for (uint32_t q = 0; q < nb; q++) B[at[chunk_of(tmp[q].node)]++] = tmp[q];
+    }
     // 4. per-word control for this tick
     for (uint32_t w : reset_now) ctl[w].clear = ~0ull;
     const bool is_cut = (t == cut_tick && cut_r > 0);
@@ -1383,6 +1425,11 @@ int gossip_engine::tick_step_a(int64_t t) {
                           (c.keep != ~0ull ? WF_KEEP : 0u) | (c.snap ? WF_SNAP : 0u));
         keep_any |= c.keep != ~0ull;
     }
+    if (opt_late_age > 0)  // bottom-up early exit in k_pull for tiles at least late_age ticks old
+        for (uint32_t w = 0; w < hw; w++) {
+            const uint32_t tl = w / kTileWords;
+            if (tile_alloc[tl] && t + 1 - tile_first[tl] >= opt_late_age) WF[w] |= (uint8_t)WF_LATE;
+        }
     for (uint32_t i = 0; i < ny; i++)  // k_pull leaves these words to k_pull_young
         if (YP->yt[i].flags)
             for (uint32_t q = 0; q < kTileWords; q++) WF[YP->yt[i].tile * kTileWords + q] |= (uint8_t)WF_YOUNG;
@@ -1400,6 +1447,34 @@ int gossip_engine::tick_step_a(int64_t t) {
     if (wact) HIP_TRY(hipMemsetAsync(d_live[lv], 0, (size_t)wact * 8, stream));
     unsigned long long* snap_ptr = snap_idx >= 0 ? d_scalars + 2 + 2 * snap_idx + 1 : nullptr;
     const int nxt = fcur ^ 1;
+    // births [off, off + cnt) of the staged array (all of them, or one row chunk's)
+    auto launch_births = [&](uint32_t off, uint32_t cnt) -> int {
+        if (!cnt) return GOSSIP_OK;
+        BirthArgs b;
+        b.b = d_births[slot] + off; b.nb = cnt; b.gphase = d_gphase[slot];
+        b.Fnext = d_F[nxt]; b.seen = d_seen; b.stride = stride;
+        b.gen = d_gen; b.recv = d_recv; b.effgen = d_effgen; b.sent = d_sent; b.deg = d_deg;
+        b.live = d_live[lv]; b.snap = snap_ptr; b.snap_r = snap_idx >= 0 ? snaps[snap_idx].r : 0;
+        b.nz = d_nz[nxt];
+        b.ntw = ntw;
+        b.degc = d_degc;
+        b.slot = (young && nwt) ? d_slot[nxt] : nullptr;
+        b.cap = (uint32_t)std::min<int64_t>(kSlotU16 - 1, std::max<int64_t>(1, opt_young_cap));
+        b.wt = young ? d_young[slot]->wt : nullptr;
+        b.nwt = nwt;
+        b.rowptr = d_rowptr; b.rev = d_rev;
+        b.hint_next = young ? d_hint[nxt] : nullptr;
+        b.stamp_next = hint_stamp(t);
+        k_births<<<(cnt + 255) / 256, 256, 0, stream>>>(b);
+        HIP_TRY(hipGetLastError());
+        return GOSSIP_OK;
+    };
+    // end of row chunk c on the engine stream: its exchange may start (exchange_rccl, export)
+    auto end_chunk = [&](uint32_t c) -> int {
+        if (!ev_chunk[c]) HIP_TRY(hipEventCreateWithFlags(&ev_chunk[c], hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ev_chunk[c], stream));
+        return GOSSIP_OK;
+    };
     if (wact) {
         PullArgs a;
         a.rowptr = d_rowptr; a.col = d_col; a.deg = d_deg;
@@ -1420,12 +1495,15 @@ int gossip_engine::tick_step_a(int64_t t) {
         a.noskip = (cfg.flags & GOSSIP_F_NOSKIP) ? 1u : 0u;
         a.keep_lds = keep_any ? 1u : 0u;
         a.gate_seen = opt_pull_gate ? 1u : 0u;
-        const uint64_t chunks = ((uint64_t)(v1 - v0) + 63) / 64;  // 64 nodes per wave step sequence
         // non-temporal rows iff the frontier the launch gathers from (n rows x wact live words)
         // exceeds kPullNtBytes
         const bool nt_rows = opt_pull_nt >= 0 ? opt_pull_nt == 1 : (uint64_t)n * wact * 8u > kPullNtBytes;
-        const uint32_t grid = (uint32_t)std::max<uint64_t>(
-            1, std::min<uint64_t>((chunks + 3) / 4, pull_grid_cap(nt_rows, opt_pull_grid)));
+        // blocks for rows [lo, hi): 64 nodes per wave step sequence, 4 waves per block
+        auto grid_for = [&](uint64_t lo, uint64_t hi) {
+            const uint64_t chunks = (hi - lo + 63) / 64;
+            return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((chunks + 3) / 4, pull_grid_cap(nt_rows, opt_pull_grid)));
+        };
+        const uint32_t grid = grid_for(v0, v1);
         last_nt = nt_rows ? 1u : 0u;
         last_grid = grid;
         const double avg_deg = n ? (double)nnz / n : 0.0;
@@ -1434,6 +1512,7 @@ int gossip_engine::tick_step_a(int64_t t) {
         // the 8 word-pairs of one tile); spare lanes of the wave split the peer list
         // (edge-lanes) when peers are many -- and never in DENSE mode, which gathers nothing.
         auto run_pull = [&](const PullArgs& base, bool split_edges) {
+            const uint32_t grid = grid_for(base.v0, base.n);
             for (uint32_t wb = 0; wb < wact; wb += kPullLdsWords) {
                 PullArgs c = base;
                 c.wbase = wb;
@@ -1527,14 +1606,13 @@ int gossip_engine::tick_step_a(int64_t t) {
             young_launches++;
             return GOSSIP_OK;
         };
-        if (dense) {
-            // The timed kernel in DENSE mode is the MFMA contraction; its incoming words are
-            // then consumed by k_pull (dedup/state/counters, untimed).
+        // the MFMA contraction of rows [lo, hi) (DENSE mode) into the incoming words
+        auto run_dense = [&](uint64_t lo, uint64_t hi) -> int {
             BitsArgs gm;
             gm.Ab = d_Ab; gm.FT = d_FT; gm.inc = d_inc; gm.live_prev = a.live_prev; gm.acct = d_acct;
-            gm.n = v1; gm.n_pad = n_pad; gm.kw = n_pad / 32u; gm.stride = stride;
-            gm.mb0 = v0 / kDenseTile;  // row partition: this engine's row blocks only
-            gm.mb = (std::min(v1 + kDenseTile - 1u, n_pad) - v0) / kDenseTile;
+            gm.n = (uint32_t)hi; gm.n_pad = n_pad; gm.kw = n_pad / 32u; gm.stride = stride;
+            gm.mb0 = (uint32_t)lo / kDenseTile;  // row partition: this engine's row blocks only
+            gm.mb = (std::min((uint32_t)hi + kDenseTile - 1u, n_pad) - (uint32_t)lo) / kDenseTile;
             gm.nt = wact / 4u;
             const uint32_t nst = n_pad / kStageK;
             uint32_t ks = 1;  // split K until the chip has ~2 tiles per CU (>= 2 stages per split)
@@ -1544,6 +1622,39 @@ int gossip_engine::tick_step_a(int64_t t) {
             gm.total = gm.mb * gm.nt * ks;
             k_dense_bits<<<(gm.total + 7u) / 8u * 8u, 512, 0, stream>>>(gm);
             HIP_TRY(hipGetLastError());
+            return GOSSIP_OK;
+        };
+        if (nchunks > 1) {
+            // Pipelined exchange: pull (+ the MFMA contraction) and births per row chunk, each
+            // chunk closed by its event so that its exchange overlaps the next chunk.  The pull
+            // timer then spans the whole chunked compute of the tick, births included.
+            for (uint32_t c = 0; c < nchunks; c++) {
+                uint64_t lo, hi;
+                chunk_rows(row_rank, c, &lo, &hi);
+                if (hi > lo) {
+                    PullArgs ac = a;
+                    ac.v0 = (uint32_t)lo;
+                    ac.n = (uint32_t)hi;
+                    if (dense) {
+                        const int rc = run_dense(lo, hi);
+                        if (rc) return rc;
+                        ac.inc = d_inc;
+                    }
+                    run_pull(ac, !dense);
+                }
+                int rc = launch_births(cb_off[c], cb_off[c + 1] - cb_off[c]);
+                if (rc) return rc;
+                if ((rc = end_chunk(c))) return rc;
+            }
+            if (cfg.flags & GOSSIP_F_TIMING) {
+                HIP_TRY(hipEventRecord(e1, stream));
+                timers.emplace_back(e0, e1);
+            }
+        } else if (dense) {
+            // The timed kernel in DENSE mode is the MFMA contraction; its incoming words are
+            // then consumed by k_pull (dedup/state/counters, untimed).
+            const int rc = run_dense(v0, v1);
+            if (rc) return rc;
             if (cfg.flags & GOSSIP_F_TIMING) {
                 HIP_TRY(hipEventRecord(e1, stream));
                 timers.emplace_back(e0, e1);
@@ -1585,24 +1696,12 @@ int gossip_engine::tick_step_a(int64_t t) {
         pull_launches++;
         pull_bytes += 8ull * (n + 1) + 4ull * nnz + 8ull * wact * nnz + 24ull * wact * n + 16ull * n;
     }
-    if (nb) {
-        BirthArgs b;
-        b.b = d_births[slot]; b.nb = nb; b.gphase = d_gphase[slot];
-        b.Fnext = d_F[nxt]; b.seen = d_seen; b.stride = stride;
-        b.gen = d_gen; b.recv = d_recv; b.effgen = d_effgen; b.sent = d_sent; b.deg = d_deg;
-        b.live = d_live[lv]; b.snap = snap_ptr; b.snap_r = snap_idx >= 0 ? snaps[snap_idx].r : 0;
-        b.nz = d_nz[nxt];
-        b.ntw = ntw;
-        b.degc = d_degc;
-        b.slot = (young && nwt) ? d_slot[nxt] : nullptr;
-        b.cap = (uint32_t)std::min<int64_t>(kSlotU16 - 1, std::max<int64_t>(1, opt_young_cap));
-        b.wt = young ? d_young[slot]->wt : nullptr;
-        b.nwt = nwt;
-        b.rowptr = d_rowptr; b.rev = d_rev;
-        b.hint_next = young ? d_hint[nxt] : nullptr;
-        b.stamp_next = hint_stamp(t);
-        k_births<<<(nb + 255) / 256, 256, 0, stream>>>(b);
-        HIP_TRY(hipGetLastError());
+    if (nchunks == 1 || !wact) {  // (chunked ticks with live words launched them per chunk)
+        for (uint32_t c = 0; c < nchunks; c++) {
+            int rc = launch_births(nchunks == 1 ? 0u : cb_off[c], nchunks == 1 ? nb : cb_off[c + 1] - cb_off[c]);
+            if (rc) return rc;
+            if ((rc = end_chunk(c))) return rc;
+        }
     }
     if (young) {  // F_next's slots hold this tick's write-sparse tiles: next tick reads them
         tile_widx.swap(new_widx);
@@ -1622,14 +1721,39 @@ int gossip_engine::tick_step_a(int64_t t) {
 }
 
 // ---- compressed row exchange (row partition) --------------------------------------------
-// A rank's message for tick t: its rows [lo, hi) of F_next, restricted to OCCUPIED 16-word tile
-// rows (the nz bits; unoccupied rows hold stale words no reader loads), plus its partial
-// liveness.  Layout in uint64 words:
+// A rank's message for tick t and row chunk c: its rows [lo, hi) of F_next (the chunk, or all
+// its rows), restricted to OCCUPIED 16-word tile rows (the nz bits; unoccupied rows hold stale
+// words no reader loads), plus -- in its last chunk only -- its partial liveness.  Layout in
+// uint64 words:
 //   [0]                      number of rows R
 //   [1, 1 + m)               nz words of rows lo..hi-1 (m = (hi - lo) * ntw)
 //   [.., + ceil((k+1)/2))    uint32 row offsets: rows of node lo+i start at offset[i] (k = hi-lo)
 //   [.., + 16 R)             the rows, node by node, tile by tile
-//   [.., + wact)             liveness words of this rank's rows
+//   [.., + wact)             liveness words of this rank's rows (last chunk / whole rows)
+// The receiver knows k and whether liveness is present from (rank, chunk), so R follows from
+// the message size: no header read-back.
+
+// Rows of rank r's chunk c: 512-row blocks (the dense tile and the row-partition granule), the
+// last chunks possibly empty; kWholeRows = all of rank r's rows.
+void gossip_engine::chunk_rows(uint32_t r, uint32_t c, uint64_t* lo, uint64_t* hi) const {
+    const uint64_t a = row_lo[r], b = row_lo[r + 1];
+    if (c == kWholeRows || nchunks <= 1) {
+        *lo = a;
+        *hi = b;
+        return;
+    }
+    const uint64_t per = ((b - a + nchunks - 1) / nchunks + 511) / 512 * 512;
+    *lo = std::min<uint64_t>(b, a + (uint64_t)c * per);
+    *hi = std::min<uint64_t>(b, *lo + per);
+}
+
+int gossip_engine::ensure_xstream() {
+    if (xstream) return GOSSIP_OK;
+    HIP_TRY(hipStreamCreateWithFlags(&xstream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&ev_xdone, hipEventDisableTiming));
+    return GOSSIP_OK;
+}
+
 struct PackLayout {
     uint64_t nz, off, rows, live, total;
 };
@@ -1706,7 +1830,8 @@ __global__ void k_or_words(const uint64_t* __restrict__ src, uint32_t n, unsigne
 
 int gossip_engine::ensure_dev(uint64_t*& p, uint64_t& cap, uint64_t words) {
     if (words <= cap) return GOSSIP_OK;
-    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(hipStreamSynchronize(stream));  // (rare: growth) both streams may still read p
+    if (xstream) HIP_TRY(hipStreamSynchronize(xstream));
     hipFree(p);
     p = nullptr;
     cap = std::max<uint64_t>(words, cap + cap / 2);
@@ -1714,118 +1839,129 @@ int gossip_engine::ensure_dev(uint64_t*& p, uint64_t& cap, uint64_t words) {
     return GOSSIP_OK;
 }
 
-// Pack this rank's rows of F_next (after this tick's pull and births) into d_msg; msg_words = size.
-int gossip_engine::pack_rows(int64_t t) {
+// Pack this rank's rows of chunk c of F_next (after the chunk's pull and births) into d_msg on
+// stream s; msg_words = size.  (One host wait: the row count sizes the message.)
+int gossip_engine::pack_rows(int64_t t, uint32_t c, hipStream_t s) {
     const int nxt = fcur ^ 1, lv = (int)(t % 3);
-    const uint64_t k = v1 - v0;
-    const uint32_t wact = hw;
-    int rc = ensure_dev(d_msg, msg_cap, pack_layout(k, ntw, 0, wact).rows);
+    uint64_t lo, hi;
+    chunk_rows(row_rank, c, &lo, &hi);
+    const uint64_t k = hi - lo;
+    const uint32_t wlive = (c == kWholeRows || c + 1 >= nchunks) ? hw : 0u;  // liveness: last chunk
+    int rc = ensure_dev(d_msg, msg_cap, pack_layout(k, ntw, 0, wlive).rows);
     if (rc) return rc;
     if (k + 1 > cnt_cap) {
-        HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipStreamSynchronize(s));
         hipFree(d_cnt);
         cnt_cap = k + 1;
         HIP_TRY(hipMalloc(&d_cnt, cnt_cap * 4));
     }
-    const PackLayout L0 = pack_layout(k, ntw, 0, wact);
+    const PackLayout L0 = pack_layout(k, ntw, 0, wlive);
     uint32_t* off = reinterpret_cast<uint32_t*>(d_msg + L0.off);
-    k_pack_count<<<(uint32_t)((k + 1 + 255) / 256), 256, 0, stream>>>(d_nz[nxt] + (uint64_t)v0 * ntw, k, ntw,
-                                                                      d_msg + L0.nz, d_cnt);
+    k_pack_count<<<(uint32_t)((k + 1 + 255) / 256), 256, 0, s>>>(d_nz[nxt] + lo * ntw, k, ntw, d_msg + L0.nz, d_cnt);
     HIP_TRY(hipGetLastError());
     size_t tmp = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d_cnt, off, (int)(k + 1), stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d_cnt, off, (int)(k + 1), s));
     if (tmp > scan_tmp_bytes) {
-        HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipStreamSynchronize(s));
         hipFree(d_scan_tmp);
         scan_tmp_bytes = tmp;
         HIP_TRY(hipMalloc(&d_scan_tmp, tmp));
     }
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(d_scan_tmp, tmp, d_cnt, off, (int)(k + 1), stream));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(d_scan_tmp, tmp, d_cnt, off, (int)(k + 1), s));
     uint32_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, off + k, 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    const PackLayout L = pack_layout(k, ntw, total, wact);
+    HIP_TRY(hipMemcpyAsync(&total, off + k, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const PackLayout L = pack_layout(k, ntw, total, wlive);
     // (the layout's header parts do not depend on the row count: grow keeping them)
     if (L.total > msg_cap) {
         uint64_t* nm = nullptr;
         HIP_TRY(hipMalloc(&nm, L.total * 8));
-        HIP_TRY(hipMemcpyAsync(nm, d_msg, L.rows * 8, hipMemcpyDeviceToDevice, stream));
-        HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipMemcpyAsync(nm, d_msg, L.rows * 8, hipMemcpyDeviceToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));
         hipFree(d_msg);
         d_msg = nm;
         msg_cap = L.total;
         off = reinterpret_cast<uint32_t*>(d_msg + L.off);
     }
     const unsigned long long hdr = total;
-    HIP_TRY(hipMemcpyAsync(d_msg, &hdr, 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_msg, &hdr, 8, hipMemcpyHostToDevice, s));
     if (total) {
         const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((k + 3) / 4, 4096));
-        k_move_rows<true><<<g, 256, 0, stream>>>(d_F[nxt], stride, v0, k, d_msg + L.nz, ntw, off, d_msg + L.rows);
+        k_move_rows<true><<<g, 256, 0, s>>>(d_F[nxt], stride, lo, k, d_msg + L.nz, ntw, off, d_msg + L.rows);
         HIP_TRY(hipGetLastError());
     }
-    if (wact) HIP_TRY(hipMemcpyAsync(d_msg + L.live, d_live[lv], (size_t)wact * 8, hipMemcpyDeviceToDevice, stream));
+    if (wlive) HIP_TRY(hipMemcpyAsync(d_msg + L.live, d_live[lv], (size_t)wlive * 8, hipMemcpyDeviceToDevice, s));
     msg_words = L.total;
     exchange_bytes_out += L.total * 8;
     return GOSSIP_OK;
 }
 
-// Unpack rank r's message (device buffer) into this engine's F_next, nz_next and liveness.
-int gossip_engine::unpack_rows(int64_t t, uint32_t r, const uint64_t* msg, uint64_t words) {
+// Unpack rank r's message of chunk c (device buffer, `words` long) into this engine's F_next,
+// nz_next and (last chunk) liveness, on stream s.  No host wait.
+int gossip_engine::unpack_rows(int64_t t, uint32_t r, uint32_t c, const uint64_t* msg, uint64_t words, hipStream_t s) {
     const int nxt = fcur ^ 1, lv = (int)(t % 3);
-    const uint64_t lo = row_lo[r], k = row_lo[r + 1] - row_lo[r];
-    const uint32_t wact = hw;
-    unsigned long long total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, msg, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    const PackLayout L = pack_layout(k, ntw, total, wact);
-    if (L.total != words) return set_error(GOSSIP_EINVAL, "row exchange: message of rank " + std::to_string(r) +
-                                                          " has the wrong size (ranks diverged?)");
-    HIP_TRY(hipMemcpyAsync(d_nz[nxt] + lo * ntw, msg + L.nz, (size_t)k * ntw * 8, hipMemcpyDeviceToDevice, stream));
+    uint64_t lo, hi;
+    chunk_rows(r, c, &lo, &hi);
+    const uint64_t k = hi - lo;
+    const uint32_t wlive = (c == kWholeRows || c + 1 >= nchunks) ? hw : 0u;
+    const PackLayout L0 = pack_layout(k, ntw, 0, wlive);
+    if (words < L0.total || (words - L0.total) % 16u)
+        return set_error(GOSSIP_EINVAL, "row exchange: message of rank " + std::to_string(r) +
+                                            " has the wrong size (ranks diverged?)");
+    const uint64_t total = (words - L0.total) / 16u;
+    const PackLayout L = pack_layout(k, ntw, total, wlive);
+    if (k) HIP_TRY(hipMemcpyAsync(d_nz[nxt] + lo * ntw, msg + L.nz, (size_t)k * ntw * 8, hipMemcpyDeviceToDevice, s));
     if (total) {
         const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((k + 3) / 4, 4096));
-        k_move_rows<false><<<g, 256, 0, stream>>>(d_F[nxt], stride, lo, k, msg + L.nz, ntw,
-                                                  reinterpret_cast<const uint32_t*>(msg + L.off),
-                                                  const_cast<uint64_t*>(msg + L.rows));
+        k_move_rows<false><<<g, 256, 0, s>>>(d_F[nxt], stride, lo, k, msg + L.nz, ntw,
+                                             reinterpret_cast<const uint32_t*>(msg + L.off),
+                                             const_cast<uint64_t*>(msg + L.rows));
         HIP_TRY(hipGetLastError());
     }
-    if (wact) {
-        k_or_words<<<(wact + 255) / 256, 256, 0, stream>>>(msg + L.live, wact, d_live[lv]);
+    if (wlive) {
+        k_or_words<<<(wlive + 255) / 256, 256, 0, s>>>(msg + L.live, wlive, d_live[lv]);
         HIP_TRY(hipGetLastError());
     }
     exchange_bytes_in += words * 8;
     return GOSSIP_OK;
 }
 
-// Row partition over RCCL: every rank packs its occupied rows, the message sizes are
-// all-gathered, then each rank's message is broadcast (an all-gather with per-rank sizes) and
-// unpacked by the others -- on the engine's stream.
+// Row partition over RCCL, pipelined: for every row chunk, once the engine stream has pulled it
+// (ev_chunk[c]), the exchange stream packs it, all-gathers the message sizes (and chunk counts),
+// broadcasts every rank's message (an all-gather with per-rank sizes) and unpacks the others'
+// chunk c -- while the engine stream already pulls chunk c + 1.  The engine stream joins the
+// exchange stream before the tick's liveness read-back (tick_step_b).
 int gossip_engine::exchange_rccl(int64_t t) {
-    int rc = pack_rows(t);
+    int rc = ensure_xstream();
     if (rc) return rc;
-    int rc2 = ensure_dev(d_sizes, sizes_cap, row_count);
-    if (rc2) return rc2;
-    const unsigned long long mine = msg_words;
-    HIP_TRY(hipMemcpyAsync(d_sizes + row_rank, &mine, 8, hipMemcpyHostToDevice, stream));
-    NCCL_TRY(ncclAllGather(d_sizes + row_rank, d_sizes, 1, ncclUint64, comm, stream));
-    std::vector<unsigned long long> sz(row_count);
-    HIP_TRY(hipMemcpyAsync(sz.data(), d_sizes, row_count * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    uint64_t tot = 0;
-    std::vector<uint64_t> at(row_count);
-    for (uint32_t r = 0; r < row_count; r++) {
-        at[r] = tot;
-        tot += r == row_rank ? 0 : sz[r];
+    if ((rc = ensure_dev(d_sizes, sizes_cap, 2 * row_count))) return rc;
+    std::vector<unsigned long long> sz(2 * row_count);
+    for (uint32_t c = 0; c < nchunks; c++) {
+        HIP_TRY(hipStreamWaitEvent(xstream, ev_chunk[c], 0));
+        if ((rc = pack_rows(t, c, xstream))) return rc;
+        const unsigned long long mine[2] = {msg_words, nchunks};
+        HIP_TRY(hipMemcpyAsync(d_sizes + 2 * row_rank, mine, 16, hipMemcpyHostToDevice, xstream));
+        NCCL_TRY(ncclAllGather(d_sizes + 2 * row_rank, d_sizes, 2, ncclUint64, comm, xstream));
+        HIP_TRY(hipMemcpyAsync(sz.data(), d_sizes, 2 * row_count * 8, hipMemcpyDeviceToHost, xstream));
+        HIP_TRY(hipStreamSynchronize(xstream));
+        uint64_t tot = 0;
+        std::vector<uint64_t> at(row_count);
+        for (uint32_t r = 0; r < row_count; r++) {
+            if (sz[2 * r + 1] != nchunks)
+                return set_error(GOSSIP_EINVAL, "row exchange: ranks use different xchunks options");
+            at[r] = tot;
+            tot += r == row_rank ? 0 : sz[2 * r];
+        }
+        if ((rc = ensure_dev(d_recv_msgs, recv_cap, std::max<uint64_t>(tot, 1)))) return rc;
+        NCCL_TRY(ncclGroupStart());
+        for (uint32_t r = 0; r < row_count; r++) {
+            uint64_t* buf = r == row_rank ? d_msg : d_recv_msgs + at[r];
+            NCCL_TRY(ncclBroadcast(buf, buf, sz[2 * r], ncclUint64, (int)r, comm, xstream));
+        }
+        NCCL_TRY(ncclGroupEnd());
+        for (uint32_t r = 0; r < row_count; r++)
+            if (r != row_rank && (rc = unpack_rows(t, r, c, d_recv_msgs + at[r], sz[2 * r], xstream))) return rc;
     }
-    rc = ensure_dev(d_recv_msgs, recv_cap, std::max<uint64_t>(tot, 1));
-    if (rc) return rc;
-    NCCL_TRY(ncclGroupStart());
-    for (uint32_t r = 0; r < row_count; r++) {
-        uint64_t* buf = r == row_rank ? d_msg : d_recv_msgs + at[r];
-        NCCL_TRY(ncclBroadcast(buf, buf, sz[r], ncclUint64, (int)r, comm, stream));
-    }
-    NCCL_TRY(ncclGroupEnd());
-    for (uint32_t r = 0; r < row_count; r++)
-        if (r != row_rank && (rc = unpack_rows(t, r, d_recv_msgs + at[r], sz[r]))) return rc;
     return GOSSIP_OK;
 }
 
@@ -1836,6 +1972,10 @@ int gossip_engine::tick_step_b(int64_t t) {
     if (comm) {
         int rc = exchange_rccl(t);
         if (rc) return rc;
+    }
+    if (xstream) {  // the unpacked rows and liveness precede the read-back and the next pull
+        HIP_TRY(hipEventRecord(ev_xdone, xstream));
+        HIP_TRY(hipStreamWaitEvent(stream, ev_xdone, 0));
     }
     // 6. liveness read-back (consumed kLag ticks later)
     {
@@ -1957,6 +2097,8 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_pull_gate = env_option("GOSSIP_PULL_GATE", 1);
         e->opt_young_waves = env_option("GOSSIP_YOUNG_WAVES", 4);
         e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
+        e->opt_xchunks = env_option("GOSSIP_XCHUNKS", 4);
+        e->opt_late_age = env_option("GOSSIP_LATE_AGE", 0);
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
         e->dense = cfg->mode == GOSSIP_MODE_DENSE;
         e->handshake = (cfg->flags & GOSSIP_F_HANDSHAKE) != 0;
@@ -2162,21 +2304,26 @@ int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end
             for (uint32_t r = 1; r < count; r++)
                 if (es[r]->hw != e0->hw || es[r]->stride != e0->stride || es[r]->fcur != e0->fcur)
                     return set_error(GOSSIP_EINVAL, "row partition engines diverged (different inputs?)");
-            // the compressed exchange of the RCCL backend, with device-to-device reads
-            for (uint32_t r = 0; r < count; r++) {
-                HIP_TRY(hipSetDevice(es[r]->device));
-                int rc = es[r]->pack_rows(t);
-                if (rc) return rc;
-                HIP_TRY(hipStreamSynchronize(es[r]->stream));
-            }
-            for (uint32_t d = 0; d < count; d++) {
-                HIP_TRY(hipSetDevice(es[d]->device));
+            // the compressed exchange of the RCCL backend, chunk by chunk, with device-to-device
+            // reads (the ranks already ran one after another, so nothing overlaps here)
+            for (uint32_t r = 1; r < count; r++)
+                if (es[r]->nchunks != e0->nchunks) return set_error(GOSSIP_EINVAL, "ranks use different xchunks options");
+            for (uint32_t c = 0; c < e0->nchunks; c++) {
                 for (uint32_t r = 0; r < count; r++) {
-                    if (r == d) continue;
-                    int rc = es[d]->unpack_rows(t, r, es[r]->d_msg, es[r]->msg_words);
+                    HIP_TRY(hipSetDevice(es[r]->device));
+                    int rc = es[r]->pack_rows(t, c, es[r]->stream);
                     if (rc) return rc;
+                    HIP_TRY(hipStreamSynchronize(es[r]->stream));
                 }
-                HIP_TRY(hipStreamSynchronize(es[d]->stream));
+                for (uint32_t d = 0; d < count; d++) {
+                    HIP_TRY(hipSetDevice(es[d]->device));
+                    for (uint32_t r = 0; r < count; r++) {
+                        if (r == d) continue;
+                        int rc = es[d]->unpack_rows(t, r, c, es[r]->d_msg, es[r]->msg_words, es[d]->stream);
+                        if (rc) return rc;
+                    }
+                    HIP_TRY(hipStreamSynchronize(es[d]->stream));
+                }
             }
             for (uint32_t r = 0; r < count; r++) {
                 HIP_TRY(hipSetDevice(es[r]->device));
@@ -2230,6 +2377,13 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
         if (value < 0) return set_error(GOSSIP_EINVAL, "mem_limit >= 0 bytes");
         if (e->have_sched) return set_error(GOSSIP_ESTATE, "mem_limit: set before the schedule");
         e->opt_mem_limit = value;
+    } else if (k == "late_age") {
+        if (value < 0 || value > 1000) return set_error(GOSSIP_EINVAL, "late_age: 0 (off) .. 1000 ticks");
+        e->opt_late_age = value;
+    } else if (k == "xchunks") {
+        if (value < 1 || value > (int64_t)gossip_engine::kMaxChunks) return set_error(GOSSIP_EINVAL, "xchunks: 1 .. 16 row chunks");
+        if (e->tick_open) return set_error(GOSSIP_ESTATE, "xchunks: not between tick_begin and tick_end");
+        e->opt_xchunks = value;
     } else if (k == "dense_min_tiles") {
         if (value < 1) return set_error(GOSSIP_EINVAL, "dense_min_tiles >= 1");
         e->opt_dense_min_tiles = value;
@@ -2260,40 +2414,76 @@ int gossip_engine_tick_begin(gossip_engine* e) {
             e->done = true;
             return 1;
         }
+        // enqueued only: the exports wait for their row chunks (ev_chunk) on the exchange stream
         if ((rc = e->tick_step_a(e->cur))) return rc;
-        if ((rc = e->pack_rows(e->cur))) return rc;
-        HIP_TRY(hipStreamSynchronize(e->stream));
+        if ((rc = e->ensure_xstream())) return rc;
     } catch (const std::bad_alloc&) {
         return set_error(GOSSIP_ENOMEM, "host allocation failed");
     }
+    e->packed_tick = -1;
     e->tick_open = true;
     return GOSSIP_OK;
 }
 
-int gossip_engine_exchange_export(gossip_engine* e, void* buf, uint64_t cap_bytes, uint64_t* bytes) {
+int gossip_engine_exchange_chunks(const gossip_engine* e) {
+    if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    return e->row_count > 1 ? (int)std::min<int64_t>(gossip_engine::kMaxChunks, std::max<int64_t>(1, e->opt_xchunks)) : 1;
+}
+
+static int export_message(gossip_engine* e, uint32_t chunk, void* buf, uint64_t cap_bytes, uint64_t* bytes) {
     int rc = check_stepping(e);
     if (rc) return rc;
     if (!e->tick_open) return set_error(GOSSIP_ESTATE, "exchange_export outside tick_begin/tick_end");
+    if (chunk != gossip_engine::kWholeRows && chunk >= e->nchunks)
+        return set_error(GOSSIP_EINVAL, "exchange_export_chunk: chunk >= gossip_engine_exchange_chunks");
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->packed_tick != e->cur || e->packed_chunk != chunk) {  // pack once per (tick, chunk)
+        const uint32_t after = chunk == gossip_engine::kWholeRows ? e->nchunks - 1u : chunk;
+        HIP_TRY(hipStreamWaitEvent(e->xstream, e->ev_chunk[after], 0));
+        if ((rc = e->pack_rows(e->cur, chunk, e->xstream))) return rc;
+        e->packed_tick = e->cur;
+        e->packed_chunk = chunk;
+    }
     if (bytes) *bytes = e->msg_words * 8;
     if (!buf) return GOSSIP_OK;
     if (cap_bytes < e->msg_words * 8) return set_error(GOSSIP_EINVAL, "export buffer too small");
-    HIP_TRY(hipSetDevice(e->device));
-    HIP_TRY(hipMemcpy(buf, e->d_msg, e->msg_words * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(buf, e->d_msg, e->msg_words * 8, hipMemcpyDeviceToHost, e->xstream));
+    HIP_TRY(hipStreamSynchronize(e->xstream));
     return GOSSIP_OK;
 }
 
-int gossip_engine_exchange_import(gossip_engine* e, uint32_t rank, const void* buf, uint64_t bytes) {
+static int import_message(gossip_engine* e, uint32_t rank, uint32_t chunk, const void* buf, uint64_t bytes) {
     int rc = check_stepping(e);
     if (rc) return rc;
     if (!e->tick_open) return set_error(GOSSIP_ESTATE, "exchange_import outside tick_begin/tick_end");
     if (rank >= e->row_count || rank == e->row_rank || !buf || bytes % 8)
         return set_error(GOSSIP_EINVAL, "exchange_import: bad rank or buffer");
+    if (chunk != gossip_engine::kWholeRows && chunk >= e->nchunks)
+        return set_error(GOSSIP_EINVAL, "exchange_import_chunk: chunk >= gossip_engine_exchange_chunks");
     HIP_TRY(hipSetDevice(e->device));
     if ((rc = e->ensure_dev(e->d_recv_msgs, e->recv_cap, std::max<uint64_t>(bytes / 8, 1)))) return rc;
-    HIP_TRY(hipMemcpyAsync(e->d_recv_msgs, buf, bytes, hipMemcpyHostToDevice, e->stream));
-    if ((rc = e->unpack_rows(e->cur, rank, e->d_recv_msgs, bytes / 8))) return rc;
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_recv_msgs, buf, bytes, hipMemcpyHostToDevice, e->xstream));
+    if ((rc = e->unpack_rows(e->cur, rank, chunk, e->d_recv_msgs, bytes / 8, e->xstream))) return rc;
+    HIP_TRY(hipStreamSynchronize(e->xstream));  // (the receive buffer is reused by the next import)
     return GOSSIP_OK;
+}
+
+int gossip_engine_exchange_export(gossip_engine* e, void* buf, uint64_t cap_bytes, uint64_t* bytes) {
+    return export_message(e, gossip_engine::kWholeRows, buf, cap_bytes, bytes);
+}
+
+int gossip_engine_exchange_import(gossip_engine* e, uint32_t rank, const void* buf, uint64_t bytes) {
+    return import_message(e, rank, gossip_engine::kWholeRows, buf, bytes);
+}
+
+int gossip_engine_exchange_export_chunk(gossip_engine* e, uint32_t chunk, void* buf, uint64_t cap_bytes,
+                                        uint64_t* bytes) {
+    return export_message(e, chunk, buf, cap_bytes, bytes);
+}
+
+int gossip_engine_exchange_import_chunk(gossip_engine* e, uint32_t rank, uint32_t chunk, const void* buf,
+                                        uint64_t bytes) {
+    return import_message(e, rank, chunk, buf, bytes);
 }
 
 int gossip_engine_tick_end(gossip_engine* e) {

@@ -46,7 +46,8 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 __device__ __forceinline__ uint32_t wave_count(bool c) { return (uint32_t)__popcll(__ballot(c)); }
 
 // WF_YOUNG: the word belongs to a young tile, which k_pull_young owns this tick (young_kernel.h)
-enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u, WF_YOUNG = 16u };
+// WF_LATE: the word's tile is old enough (option late_age) for the bottom-up early exit
+enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u, WF_YOUNG = 16u, WF_LATE = 32u };
 
 constexpr uint32_t kPullLdsWords = 2048;  // words per launch: LDS liveness, new liveness, flags
 #ifndef PULL_INFLIGHT
@@ -282,13 +283,16 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                     // every F_cur bit lies inside live_prev, and seen / not-kept bits are
                     // masked out of `new`, so peers beyond covering these add nothing.
                     const uint64_t want0 = lp0 & ~s2.x & k0, want1 = lp1 & ~s2.y & k1;
+                    // late tiles (WF_LATE, set by the host from the tile's age): dense frontier
+                    // rows, few unseen bits -- stop at the first batch that covers them all
+                    const bool late = ((f0 | f1) & WF_LATE) != 0u;
                     // one lane group's worth of peers (ids in `cid`, occupancy words in `nzw`)
                     auto gchunk = [&](uint32_t cid, unsigned long long nzw, int rem) {
                         t_col += wave_count((int)gl < rem);
                         // the <= 8 occupancy bits of this pass's tiles, tested per lane by tile
                         const uint32_t nzp = (uint32_t)(nzw >> ((((w - 2u * wl) >> 4)) & 63u)) & 0xffu;
                         for (int t0 = 0; t0 < rem; t0 += kInflight) {
-                            int open = (a.noskip || !PULL_EARLY_EXIT)
+                            int open = (a.noskip || !(PULL_EARLY_EXIT || late))
                                            ? 1 : (((want0 & ~acc0) | (want1 & ~acc1)) != 0ull);
                             open |= __shfl_xor(open, 1, GRP);  // per tile (8 word-lanes)
                             open |= __shfl_xor(open, 2, GRP);

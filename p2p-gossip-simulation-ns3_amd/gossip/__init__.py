@@ -57,7 +57,8 @@ EXPORTED_SYMBOLS = (
     "gossip_rccl_unique_id", "gossip_engine_connect_rccl", "gossip_engine_group_run",
     "gossip_engine_set_option", "gossip_engine_mode", "gossip_engine_tick_begin",
     "gossip_engine_exchange_export", "gossip_engine_exchange_import", "gossip_engine_tick_end",
-    "gossip_schedule_create_philox",
+    "gossip_schedule_create_philox", "gossip_engine_exchange_chunks",
+    "gossip_engine_exchange_export_chunk", "gossip_engine_exchange_import_chunk",
 )
 
 # NS-3 5 Mbps point-to-point links (p2pnetwork.cc:113): ns per byte, PPP+IPv4+TCP(timestamp
@@ -163,6 +164,9 @@ def load_library(path: str = LIB_PATH):
         "gossip_engine_exchange_export": (C.c_int, [P, P, u64, C.POINTER(u64)]),
         "gossip_engine_exchange_import": (C.c_int, [P, u32, P, u64]),
         "gossip_engine_tick_end": (C.c_int, [P]),
+        "gossip_engine_exchange_chunks": (C.c_int, [P]),
+        "gossip_engine_exchange_export_chunk": (C.c_int, [P, u32, P, u64, C.POINTER(u64)]),
+        "gossip_engine_exchange_import_chunk": (C.c_int, [P, u32, u32, P, u64]),
         "gossip_format_event_log": (i64, [P, u64, P, u64, P, P, P, P, i64, i64, i64, i64, u32,
                                           i64, C.c_int, C.c_char_p, u64]),
         "gossip_engine_first_tick": (i64, [P]),
@@ -387,9 +391,9 @@ class Engine:
         _check(load_library().gossip_engine_connect_rccl(self._h, unique_id, len(unique_id)),
                "rccl connect")
 
-    # ---- host-staged row exchange (gossip.h): one message per rank and tick ----
+    # ---- host-staged row exchange (gossip.h): one message per rank and tick, or per row chunk --
     def tick_begin(self) -> bool:
-        """Pull + births of the next tick and pack this rank's rows; False when the run is done."""
+        """Enqueue pull + births of the next tick (row chunk by row chunk); False when done."""
         rc = load_library().gossip_engine_tick_begin(self._h)
         if rc == 1:
             return False
@@ -408,6 +412,27 @@ class Engine:
         msg = np.ascontiguousarray(msg, np.uint64)
         _check(load_library().gossip_engine_exchange_import(self._h, int(rank), _vp(msg), msg.nbytes),
                "import")
+
+    def exchange_chunks(self) -> int:
+        """Row chunks of the pipelined exchange (option xchunks; 1 without a row partition)."""
+        rc = load_library().gossip_engine_exchange_chunks(self._h)
+        _check(min(rc, 0), "exchange chunks")
+        return rc
+
+    def exchange_export_chunk(self, chunk: int) -> np.ndarray:
+        """This rank's message of row chunk `chunk` (waits for that chunk only)."""
+        lib = load_library()
+        n = C.c_uint64()
+        _check(lib.gossip_engine_exchange_export_chunk(self._h, int(chunk), None, 0, C.byref(n)), "export size")
+        buf = np.empty(n.value // 8, np.uint64)
+        _check(lib.gossip_engine_exchange_export_chunk(self._h, int(chunk), _vp(buf), buf.nbytes, C.byref(n)),
+               "export")
+        return buf
+
+    def exchange_import_chunk(self, rank: int, chunk: int, msg: np.ndarray):
+        msg = np.ascontiguousarray(msg, np.uint64)
+        _check(load_library().gossip_engine_exchange_import_chunk(self._h, int(rank), int(chunk), _vp(msg),
+                                                                   msg.nbytes), "import")
 
     def tick_end(self):
         _check(load_library().gossip_engine_tick_end(self._h), "tick end")

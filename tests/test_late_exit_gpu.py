@@ -1,0 +1,66 @@
+"""Late-tile bottom-up early exit in k_pull (option late_age, WF_LATE) against ORACLE A.
+
+For a tile at least `late_age` ticks old, k_pull stops reading a node's peer rows at the first
+batch whose OR covers every bit the node can still take (live last tick, unseen, kept): the
+remaining rows cannot change `new` (p2pnode.cc:189 -- a share already in processedShares is
+dropped), so the counters and the first-contact trace must stay bit-exact, with id groups,
+a cut inside a tick and young tiles on or off, while fewer peer rows are read.
+"""
+import numpy as np
+import pytest
+
+from cases import T0
+
+pytestmark = pytest.mark.gpu
+
+STATS = ("gen", "recv", "fwd", "sent", "processed", "peers", "sockets")
+
+
+def _engine(gossip, topo, ev, lat, t_cut, opts, flags):
+    eng = gossip.Engine(topo.num_nodes, lat, T0, t_cut, flags=flags)
+    for k, v in opts.items():
+        eng.set_option(k, v)
+    eng.set_topology(topo)
+    eng.set_schedule(ev)
+    eng.run()
+    eng.sync()
+    return eng
+
+
+@pytest.mark.parametrize("late_age,young", [(1, 0), (3, 0), (6, 1), (2, 1)])
+def test_late_exit_matches_oracle(gossip, oracle, late_age, young):
+    n = 6000
+    topo = gossip.Topology.gnp(n, 16.0 / (n - 1), 91, gossip.TOPO_SKIP)
+    lat = gossip.milliseconds_to_ns(5.0)
+    t_cut = gossip.seconds_to_ns(7.37)  # a cut inside a tick: keep masks on late words
+    ev = gossip.make_schedule(n, 92, T0, t_cut, id_mask=0x3FFF)  # id groups
+    eng = _engine(gossip, topo, ev, lat, t_cut, dict(late_age=late_age, young=young),
+                  gossip.F_TRACE | gossip.F_TILE_PER_TICK)
+    st = eng.stats()
+    a, b = topo.links()
+    r = oracle.run_replay(n, lat, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=True)
+    for k in STATS:
+        assert np.array_equal(getattr(st, k), getattr(r, k)), (late_age, k)
+    node, sid, tick, hop, via = eng.trace()
+    tn, ti, tt, th, tv = r.trace
+    ek, ok = np.lexsort((sid, node)), np.lexsort((ti, tn))
+    assert np.array_equal(node[ek], tn[ok]) and np.array_equal(sid[ek], ti[ok])
+    assert np.array_equal(tick[ek], tt[ok] // lat) and np.array_equal(hop[ek], th[ok])
+    eng.close()
+
+
+def test_late_exit_reads_fewer_rows(gossip):
+    # 200k nodes, degree 16: late tiles (dense frontier, few unseen bits) stop after one batch
+    n = 200_000
+    topo = gossip.Topology.gnp(n, 16.0 / (n - 1), 93, gossip.TOPO_SKIP, threads=16)
+    lat = gossip.milliseconds_to_ns(5.0)
+    t_cut = gossip.seconds_to_ns(5.4)
+    ev = gossip.make_schedule(n, 94, T0, t_cut)
+    runs = {}
+    for late in (0, 6):
+        eng = _engine(gossip, topo, ev, lat, t_cut, dict(late_age=late, young=0), 0)
+        runs[late] = (eng.stats(), eng.counters())
+        eng.close()
+    for k in STATS:
+        assert np.array_equal(getattr(runs[0][0], k), getattr(runs[6][0], k)), k
+    assert runs[6][1].pull_pair_edges < runs[0][1].pull_pair_edges

@@ -6,7 +6,10 @@ of the test box; torch.distributed gloo as the transport / control plane):
 * row partition with the host-staged exchange: each process owns a block of node rows and, every
   tick, exports its packed occupied frontier rows (gossip_engine_exchange_export), all-gathers
   the messages over gloo and imports the other rank's (the same messages the RCCL backend
-  broadcasts over xGMI).
+  broadcasts over xGMI);
+* the same, pipelined ("rows-*-chunked"): per row chunk, export_chunk waits only for that chunk
+  of the GPU's pull, so chunk c travels while the GPU pulls chunk c + 1 -- the RCCL backend's
+  overlap, on the engine's exchange stream.
 
 Both must sum to the single engine's counters bit for bit, with forced id collisions for the
 shards and the dense (MFMA) path for the rows.
@@ -41,8 +44,8 @@ def _inputs(gossip, case):
         t_cut = gossip.seconds_to_ns(9.0)
         ev = gossip.make_schedule(n, 22, T0, t_cut, id_mask=0x3FFF)
         return n, topo, t_cut, ev, gossip.MODE_CSR
-    n = 2048
-    dense = case == "rows-dense"
+    n = 2048 if not case.endswith("chunked") else 4096
+    dense = case.startswith("rows-dense")
     topo = gossip.Topology.gnp(n, 0.3 if dense else 0.01, 23, gossip.TOPO_EXACT)
     t_cut = gossip.seconds_to_ns(6.3)
     ev = gossip.make_schedule(n, 24, T0, t_cut)
@@ -77,14 +80,22 @@ def _worker(rank, port, q, case):
             eng.set_row_partition(rank, WORLD)
             eng.set_topology(topo)
             eng.set_schedule(ev)
+            chunked = case.endswith("chunked")
+            if chunked:
+                eng.set_option("xchunks", 3)
+                assert eng.exchange_chunks() == 3
             ticks = 0
             while eng.tick_begin():
-                mine = eng.exchange_export()
-                msgs = [None] * WORLD
-                dist.all_gather_object(msgs, mine)
-                for r in range(WORLD):
-                    if r != rank:
-                        eng.exchange_import(r, msgs[r])
+                for c in range(eng.exchange_chunks() if chunked else 1):
+                    mine = eng.exchange_export_chunk(c) if chunked else eng.exchange_export()
+                    msgs = [None] * WORLD
+                    dist.all_gather_object(msgs, mine)
+                    for r in range(WORLD):
+                        if r != rank:
+                            if chunked:
+                                eng.exchange_import_chunk(r, c, msgs[r])
+                            else:
+                                eng.exchange_import(r, msgs[r])
                 eng.tick_end()
                 ticks += 1
             eng.sync()
@@ -99,7 +110,7 @@ def _worker(rank, port, q, case):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", ["shards", "rows-csr", "rows-dense"])
+@pytest.mark.parametrize("case", ["shards", "rows-csr", "rows-dense", "rows-csr-chunked", "rows-dense-chunked"])
 def test_world2_processes_match_single_engine(gossip, case):
     import torch.multiprocessing as mp
 

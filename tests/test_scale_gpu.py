@@ -155,6 +155,8 @@ def test_c4_sample_matches_oracle_a(gossip, oracle, c4):
         ("nt rows, 3-block grid", (("pull_nt", 1), ("pull_grid", 3))),
         ("64 word-lanes", (("pull_lpw", 64),)),
         ("every live seen pair read (no occupancy gate)", (("pull_gate", 0),)),
+        ("bottom-up early exit on every tile", (("late_age", 1),)),
+        ("bottom-up early exit on tiles >= 4 ticks old, nt rows", (("late_age", 4), ("pull_nt", 1))),
     ]
     for name, opts in variants:
         st, c = _run(gossip, topo, ev, W.T0_NS, t_cut, options=opts, max_words=16)
