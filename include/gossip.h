@@ -366,6 +366,18 @@ int64_t gossip_format_event_log(const gossip_topology* t, uint64_t num_events,
                                 int64_t ns_per_byte, uint32_t header_bytes,
                                 int64_t send_defer_ns, int with_time, char* buf,
                                 uint64_t buf_len);
+/* NetAnim XML of SetupNetAnim (p2pnetwork.cc:153-190): the node grid, descriptions, colours
+ * and links, plus -- packets != 0, EnablePacketMetadata(true) at :187 -- one <p> record per
+ * gossip Send (p2pnode.cc:140) derived from a run's first-contact trace as in the event log
+ * (fbTx/lbTx/fbRx/lbRx in seconds from the link model: latency, send deferral and
+ * (len(message) + header_bytes) x ns_per_byte; meta-info = the Share::ToString() payload).  Needs
+ * unique share ids.  TCP handshake, ACK and REGISTER segments are not recorded.  Writes into
+ * buf (NUL-terminated) and returns the full length; buf=NULL sizes it. */
+int64_t gossip_format_netanim(const gossip_topology* t, uint64_t num_events, const gossip_gen_event* ev,
+                              uint64_t num_trace, const uint32_t* tr_node, const uint32_t* tr_share_id,
+                              const uint32_t* tr_hop, int64_t latency_ns, int64_t t_cut_ns,
+                              int64_t ns_per_byte, uint32_t header_bytes, int64_t send_defer_ns,
+                              int packets, char* buf, uint64_t buf_len);
 
 /* ------------------------------------------------------------------------------------
  * Report: the exact NS_LOG_INFO lines of PrintStatistics (p2pnetwork.cc:255-284) and

@@ -25,6 +25,7 @@
 // address (HandleAccept, p2pnode.cc:73) and the "has no peers" lines of generations before
 // t_start (p2pnode.cc:110), which are not in a counted schedule.
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <sstream>
 #include <string>
@@ -179,6 +180,105 @@ extern "C" int64_t gossip_format_event_log(const gossip_topology* t, uint64_t m,
             buf[k] = 0;
         }
         return (int64_t)s.size();
+    } catch (const std::bad_alloc&) {
+        return set_error(GOSSIP_ENOMEM, "host allocation failed");
+    }
+}
+
+// NetAnim XML (SetupNetAnim, p2pnetwork.cc:153-190), with the packet records that
+// EnablePacketMetadata(true) (:187) asks for.  Topology part: nodes on a ceil(sqrt(n)) grid 100
+// units apart, "Node i" descriptions, colours by |peers| when SetupNetAnim runs -- Start() calls it
+// before makeconnections, so every node still has 0 peers and is blue (the reference's own
+// behaviour) -- and one link per connection key.  Packet part (packets != 0): one <p> record per
+// gossip Send (p2pnode.cc:140), from the first-contact trace exactly as the event log derives its
+// "sending share" lines: first byte on the wire fbTx = first contact + send deferral, last byte
+// lbTx = fbTx + (len(message) + header bytes) x ns_per_byte, fbRx / lbRx = + latency, times in
+// seconds; meta-info = the application payload Share::ToString() (p2pnode.cc:6-11).  Not recorded:
+// the TCP handshake, ACKs and REGISTER segments.  Element layout after ns-3's AnimationInterface;
+// no NS-3 run is available to pin the exact attribute formatting (visual parity).
+extern "C" int64_t gossip_format_netanim(const gossip_topology* t, uint64_t m, const gossip_gen_event* ev,
+                                         uint64_t nt, const uint32_t* tr_node, const uint32_t* tr_id,
+                                         const uint32_t* tr_hop, int64_t latency_ns, int64_t t_cut_ns,
+                                         int64_t ns_per_byte, uint32_t header_bytes, int64_t send_defer_ns,
+                                         int packets, char* buf, uint64_t buf_len) {
+    if (!t || (m && !ev) || (nt && (!tr_node || !tr_id || !tr_hop))) return set_error(GOSSIP_EINVAL, "NULL argument");
+    if (latency_ns <= 0) return set_error(GOSSIP_EINVAL, "latency must be positive");
+    try {
+        const uint32_t n = t->n;
+        std::ostringstream os;
+        const uint32_t grid = (uint32_t)std::ceil(std::sqrt((double)n));
+        const uint32_t rows = grid ? (n + grid - 1) / grid : 0;
+        os << "<anim ver=\"netanim-3.108\" filetype=\"animation\" >\n";
+        os << "<topology minX = \"0\" minY = \"0\" maxX = \"" << (grid ? 100u * (grid - 1) : 0u)
+           << "\" maxY = \"" << (rows ? 100u * (rows - 1) : 0u) << "\">\n";
+        for (uint32_t i = 0; i < n; i++)
+            os << "<node id=\"" << i << "\" sysId=\"0\" locX=\"" << 100u * (i % grid) << "\" locY=\""
+               << 100u * (i / grid) << "\" />\n";
+        for (uint32_t i = 0; i < n; i++) {
+            os << "<nu p=\"c\" t=\"0\" id=\"" << i << "\" r=\"0\" g=\"0\" b=\"255\" />\n";
+            os << "<nu p=\"d\" t=\"0\" id=\"" << i << "\" descr=\"Node " << i << "\" />\n";
+        }
+        for (size_t k = 0; k < t->la.size(); k++)
+            os << "<link fromId=\"" << t->la[k] << "\" toId=\"" << t->lb[k] << "\" fd=\"\" td=\"\" ld=\"\" />\n";
+        os << "</topology>\n";
+        if (packets && nt) {
+            std::vector<std::vector<uint32_t>> peers(n);  // the reference's order (see above)
+            for (size_t k = 0; k < t->la.size(); k++) {
+                auto& p = peers[t->la[k]];
+                if (std::find(p.begin(), p.end(), t->lb[k]) == p.end()) p.push_back(t->lb[k]);
+            }
+            for (size_t k = 0; k < t->la.size(); k++) peers[t->lb[k]].push_back(t->la[k]);
+            std::unordered_map<uint32_t, uint32_t> by_id;
+            by_id.reserve(m * 2 + 1);
+            for (uint64_t k = 0; k < m; k++) {
+                if (ev[k].node >= n) return set_error(GOSSIP_EINVAL, "event node out of range");
+                if (!by_id.emplace(ev[k].share_id, (uint32_t)k).second)
+                    return set_error(GOSSIP_EINVAL, "NetAnim packets need unique share ids (n <= 128,849)");
+            }
+            struct Pkt {
+                int64_t t;
+                uint32_t from, to, s;
+            };
+            std::vector<Pkt> pk;
+            std::vector<int64_t> wire(m, 0);  // serialisation of one message of share k
+            std::vector<std::string> msg(m);
+            for (uint64_t i = 0; i < nt; i++) {
+                const auto it = by_id.find(tr_id[i]);
+                if (it == by_id.end()) return set_error(GOSSIP_EINVAL, "trace names an unknown share id");
+                const uint32_t s = it->second;
+                if (tr_node[i] >= n) return set_error(GOSSIP_EINVAL, "trace node out of range");
+                if (msg[s].empty()) {
+                    std::ostringstream ms;
+                    ms << "SHARE:" << ev[s].node << ":" << ev[s].share_id << ":" << (double)ev[s].ns / 1e9;
+                    msg[s] = ms.str();
+                    wire[s] = ((int64_t)msg[s].size() + header_bytes) * ns_per_byte;
+                }
+                const int64_t tf = ev[s].ns + (int64_t)tr_hop[i] * (latency_ns + send_defer_ns + wire[s]);
+                if (tf >= t_cut_ns) continue;
+                for (uint32_t p : peers[tr_node[i]]) pk.push_back(Pkt{tf, tr_node[i], p, s});
+            }
+            std::stable_sort(pk.begin(), pk.end(), [](const Pkt& a, const Pkt& b) {
+                if (a.t != b.t) return a.t < b.t;
+                if (a.from != b.from) return a.from < b.from;
+                return a.s < b.s;
+            });
+            os.precision(9);
+            os << std::fixed;
+            for (const Pkt& q : pk) {
+                const int64_t fb = q.t + send_defer_ns, lb = fb + wire[q.s];
+                os << "<p fId=\"" << q.from << "\" fbTx=\"" << fb / 1e9 << "\" lbTx=\"" << lb / 1e9
+                   << "\" meta-info=\"" << msg[q.s] << "\" tId=\"" << q.to << "\" fbRx=\""
+                   << (fb + latency_ns) / 1e9 << "\" lbRx=\"" << (lb + latency_ns) / 1e9 << "\" />\n";
+            }
+        }
+        os << "</anim>\n";
+        const std::string out = os.str();
+        if (buf && buf_len) {
+            const uint64_t k = std::min<uint64_t>(out.size(), buf_len - 1);
+            std::memcpy(buf, out.data(), k);
+            buf[k] = 0;
+        }
+        return (int64_t)out.size();
     } catch (const std::bad_alloc&) {
         return set_error(GOSSIP_ENOMEM, "host allocation failed");
     }

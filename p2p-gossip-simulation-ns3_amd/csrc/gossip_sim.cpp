@@ -46,6 +46,7 @@ struct Options {
     bool handshake = false;            // NS-3 handshake window (GOSSIP_F_HANDSHAKE)
     bool hopBatch = false;             // hop-batched run (GOSSIP_F_HOP_BATCH)
     bool linkTiming = false;           // 5 Mbps serialisation per hop (implies --hopBatch)
+    bool noPackets = false;            // --netanim without packet records
     std::string mode = "auto";         // auto | csr | dense
     std::string dumpLinks, dumpEvents, linksIn, eventsIn, dumpTrace, netanim;
     std::string log;  // per-event NS_LOG_INFO lines ("-" = stderr, where NS_LOG writes)
@@ -64,7 +65,7 @@ void usage() {
                  "                  [--device=D] [--threads=T] [--maxWords=W] [--quiet]\n"
                  "                  [--noPeriodic] [--timing] [--handshake] [--hopBatch] [--linkTiming]\n"
                  "                  [--mode=auto|csr|dense] [--dumpLinks=F] [--dumpEvents=F]\n"
-                 "                  [--links=F] [--events=F] [--dumpTrace=F] [--netanim=F]\n"
+                 "                  [--links=F] [--events=F] [--dumpTrace=F] [--netanim=F] [--noPackets]\n"
                  "                  [--log=F|-] [--gpus=N] [--shards=S] [--layout=shards|rows]\n"
                  "                  [--memLimitMB=M] [--schedule=exact|philox]\n");
 }
@@ -129,6 +130,7 @@ bool parse(int argc, char** argv, Options& o) {
         else if (key == "dumpTrace") { if (!need()) return false; o.dumpTrace = val; }
         else if (key == "log") { if (!need()) return false; o.log = val; }
         else if (key == "netanim") { if (!need()) return false; o.netanim = val; }
+        else if (key == "noPackets") o.noPackets = true;
         else if (key == "gpus") { if (!num(d) || d < 1 || d > 64) return false; o.gpus = (int)d; }
         else if (key == "shards") { if (!num(d) || d < 0 || d > 4096) return false; o.shards = (uint32_t)d; }
         else if (key == "layout") { if (!need()) return false; o.layout = val; }
@@ -140,34 +142,6 @@ bool parse(int argc, char** argv, Options& o) {
         }
     }
     return true;
-}
-
-// SetupNetAnim (p2pnetwork.cc:153-190) as a NetAnim XML file: nodes on a ceil(sqrt(n)) grid
-// 100 units apart, "Node i" descriptions, colours by |peers| at the time SetupNetAnim runs --
-// Start() calls it before makeconnections, so every node still has 0 peers and is blue
-// (the reference's own behaviour) -- and one link per connection key.  The element layout
-// follows ns-3's AnimationInterface output; packet records (EnablePacketMetadata) are not
-// written.  Visual parity only: no NS-3 run is available to pin the format.
-bool write_netanim(const std::string& path, uint32_t n, const std::vector<uint32_t>& a,
-                   const std::vector<uint32_t>& b) {
-    FILE* f = std::fopen(path.c_str(), "w");
-    if (!f) return false;
-    const uint32_t grid = (uint32_t)std::ceil(std::sqrt((double)n));
-    const uint32_t rows = grid ? (n + grid - 1) / grid : 0;
-    std::fprintf(f, "<anim ver=\"netanim-3.108\" filetype=\"animation\" >\n");
-    std::fprintf(f, "<topology minX = \"0\" minY = \"0\" maxX = \"%u\" maxY = \"%u\">\n",
-                 grid ? 100u * (grid - 1) : 0u, rows ? 100u * (rows - 1) : 0u);
-    for (uint32_t i = 0; i < n; i++)
-        std::fprintf(f, "<node id=\"%u\" sysId=\"0\" locX=\"%u\" locY=\"%u\" />\n", i,
-                     100u * (i % grid), 100u * (i / grid));
-    for (uint32_t i = 0; i < n; i++) {
-        std::fprintf(f, "<nu p=\"c\" t=\"0\" id=\"%u\" r=\"0\" g=\"0\" b=\"255\" />\n", i);
-        std::fprintf(f, "<nu p=\"d\" t=\"0\" id=\"%u\" descr=\"Node %u\" />\n", i, i);
-    }
-    for (size_t k = 0; k < a.size(); k++)
-        std::fprintf(f, "<link fromId=\"%u\" toId=\"%u\" fd=\"\" td=\"\" ld=\"\" />\n", a[k], b[k]);
-    std::fprintf(f, "</topology>\n</anim>\n");
-    return std::fclose(f) == 0;
 }
 
 int die(const char* what) {
@@ -310,12 +284,8 @@ int main(int argc, char** argv) {
         for (size_t k = 0; f && k < a.size(); k++) std::fprintf(f, "%u %u\n", a[k], b[k]);
         if (f) std::fclose(f);
     }
-    if (!o.netanim.empty()) {
-        std::vector<uint32_t> a(gossip_topology_num_links(topo)), b(a.size());
-        gossip_topology_get_links(topo, a.data(), b.data());
-        if (!write_netanim(o.netanim, n, a, b)) { std::perror(o.netanim.c_str()); return 1; }
+    if (!o.netanim.empty())  // (the file is written after the run: it holds the run's packets)
         std::printf("NetAnim configured to save in %s\n", o.netanim.c_str());  // p2pnetwork.cc:189
-    }
     if (!o.dumpEvents.empty()) {
         std::vector<gossip_gen_event> ev(gossip_schedule_size(sched));
         gossip_schedule_get(sched, ev.data());
@@ -339,7 +309,9 @@ int main(int argc, char** argv) {
     if (o.layout != "shards" && o.layout != "rows") { usage(); return 2; }
     const bool rows = o.layout == "rows";
     cfg.max_words = o.maxWords;
-    const bool want_trace = !(o.dumpTrace.empty() && o.log.empty());
+    // (NetAnim packet records need the trace and unique ids: small runs, n <= 128,849)
+    const bool anim_packets = !o.netanim.empty() && n <= 128849u && !o.noPackets;
+    const bool want_trace = !(o.dumpTrace.empty() && o.log.empty()) || anim_packets;
     cfg.flags = (o.timing ? GOSSIP_F_TIMING : 0u) | (o.handshake ? GOSSIP_F_HANDSHAKE : 0u) |
                 (o.hopBatch ? GOSSIP_F_HOP_BATCH : 0u) | (want_trace ? GOSSIP_F_TRACE : 0u);
     if (!o.log.empty() && o.handshake) {
@@ -463,6 +435,23 @@ int main(int argc, char** argv) {
         if (!f) { std::perror(o.log.c_str()); return 1; }
         std::fwrite(buf.data(), 1, (size_t)len, f);
         if (f != stderr) std::fclose(f);
+    }
+    if (!o.netanim.empty()) {  // SetupNetAnim + EnablePacketMetadata (p2pnetwork.cc:153-190)
+        std::vector<gossip_gen_event> ev(gossip_schedule_size(sched));
+        if (!ev.empty()) gossip_schedule_get(sched, ev.data());
+        const int64_t npb = o.linkTiming ? 1600 : 0, dfr = o.linkTiming ? 1 : 0;
+        const uint32_t hdr = o.linkTiming ? 54u : 0u;
+        const int pk = anim_packets ? 1 : 0;
+        const int64_t len = gossip_format_netanim(topo, ev.size(), ev.data(), m_tr, tn.data(), ti.data(), th.data(),
+                                                  L, t_cut, npb, hdr, dfr, pk, nullptr, 0);
+        if (len < 0) return die("netanim");
+        std::string buf((size_t)len + 1, '\0');
+        gossip_format_netanim(topo, ev.size(), ev.data(), m_tr, tn.data(), ti.data(), th.data(), L, t_cut, npb, hdr,
+                              dfr, pk, &buf[0], buf.size());
+        FILE* f = std::fopen(o.netanim.c_str(), "w");
+        if (!f) { std::perror(o.netanim.c_str()); return 1; }
+        std::fwrite(buf.data(), 1, (size_t)len, f);
+        std::fclose(f);
     }
     if (!o.dumpTrace.empty()) {  // first contact per (node, shareId): tick, hop, via ReceiveShare
         const uint64_t m = m_tr;

@@ -59,6 +59,7 @@ EXPORTED_SYMBOLS = (
     "gossip_engine_exchange_export", "gossip_engine_exchange_import", "gossip_engine_tick_end",
     "gossip_schedule_create_philox", "gossip_engine_exchange_chunks",
     "gossip_engine_exchange_export_chunk", "gossip_engine_exchange_import_chunk",
+    "gossip_format_netanim",
 )
 
 # NS-3 5 Mbps point-to-point links (p2pnetwork.cc:113): ns per byte, PPP+IPv4+TCP(timestamp
@@ -167,6 +168,8 @@ def load_library(path: str = LIB_PATH):
         "gossip_engine_exchange_chunks": (C.c_int, [P]),
         "gossip_engine_exchange_export_chunk": (C.c_int, [P, u32, P, u64, C.POINTER(u64)]),
         "gossip_engine_exchange_import_chunk": (C.c_int, [P, u32, u32, P, u64]),
+        "gossip_format_netanim": (i64, [P, u64, P, u64, P, P, P, i64, i64, i64, u32, i64, C.c_int,
+                                        C.c_char_p, u64]),
         "gossip_format_event_log": (i64, [P, u64, P, u64, P, P, P, P, i64, i64, i64, i64, u32,
                                           i64, C.c_int, C.c_char_p, u64]),
         "gossip_engine_first_tick": (i64, [P]),
@@ -545,6 +548,24 @@ def format_event_log(topo: "Topology", ev: np.ndarray, trace, latency_ns: int, t
         t, body = line.split("\t", 1)
         out.append((int(t), body))
     return out
+
+
+def format_netanim(topo: "Topology", ev: np.ndarray, trace, latency_ns: int, t_cut_ns: int,
+                   link_timing=None, packets: bool = True) -> str:
+    """NetAnim XML of SetupNetAnim + EnablePacketMetadata (gossip.h, gossip_format_netanim): the
+    node grid and links, and one <p> record per gossip Send derived from the first-contact trace
+    (node, share_id, tick, hop, ...) of a run whose generation events are `ev`."""
+    lib = load_library()
+    ev = np.ascontiguousarray(ev, GEN_EVENT_DTYPE)
+    node, sid, hop = (np.ascontiguousarray(trace[k], np.uint32) for k in (0, 1, 3))
+    npb, hdr, dfr = link_timing or (0, 0, 0)
+    args = [topo._h, ev.size, _vp(ev), node.size, _vp(node), _vp(sid), _vp(hop), int(latency_ns),
+            int(t_cut_ns), int(npb), int(hdr), int(dfr), 1 if packets else 0]
+    ln = lib.gossip_format_netanim(*args, None, 0)
+    _check(ln if ln < 0 else 0, "netanim")
+    buf = C.create_string_buffer(ln + 1)
+    lib.gossip_format_netanim(*args, buf, ln + 1)
+    return buf.value.decode()
 
 
 def format_statistics(st: Stats) -> str:

@@ -34,9 +34,14 @@ def test_late_exit_matches_oracle(gossip, oracle, late_age, young):
     lat = gossip.milliseconds_to_ns(5.0)
     t_cut = gossip.seconds_to_ns(7.37)  # a cut inside a tick: keep masks on late words
     ev = gossip.make_schedule(n, 92, T0, t_cut, id_mask=0x3FFF)  # id groups
+    # a fresh tile per tick keeps the window wider than 64 words: the one-peer-walk-per-node
+    # pull (k_pull<32, 1>) that carries the exit
     eng = _engine(gossip, topo, ev, lat, t_cut, dict(late_age=late_age, young=young),
                   gossip.F_TRACE | gossip.F_TILE_PER_TICK)
     st = eng.stats()
+    base = _engine(gossip, topo, ev, lat, t_cut, dict(late_age=0, young=young), gossip.F_TILE_PER_TICK)
+    assert eng.counters().pull_pair_edges < base.counters().pull_pair_edges  # the exit was taken
+    base.close()
     a, b = topo.links()
     r = oracle.run_replay(n, lat, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=True)
     for k in STATS:
@@ -57,10 +62,10 @@ def test_late_exit_reads_fewer_rows(gossip):
     t_cut = gossip.seconds_to_ns(5.4)
     ev = gossip.make_schedule(n, 94, T0, t_cut)
     runs = {}
-    for late in (0, 6):
-        eng = _engine(gossip, topo, ev, lat, t_cut, dict(late_age=late, young=0), 0)
+    for late in (0, 4):
+        eng = _engine(gossip, topo, ev, lat, t_cut, dict(late_age=late, young=0), gossip.F_TILE_PER_TICK)
         runs[late] = (eng.stats(), eng.counters())
         eng.close()
     for k in STATS:
-        assert np.array_equal(getattr(runs[0][0], k), getattr(runs[6][0], k)), k
-    assert runs[6][1].pull_pair_edges < runs[0][1].pull_pair_edges
+        assert np.array_equal(getattr(runs[0][0], k), getattr(runs[4][0], k)), k
+    assert runs[4][1].pull_pair_edges < runs[0][1].pull_pair_edges

@@ -4,8 +4,6 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd $R
-timeout -k 10 600 python -u -m pytest tests/test_late_exit_gpu.py -x -v --timeout 300 --timeout-method thread -m gpu > gpurun_out/gpu_late.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/gpu_late.log; [ $rc -eq 0 ] || exit 1
 B="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline"
 run() {  # name, env...
     local name=$1; shift
@@ -15,3 +13,5 @@ run() {  # name, env...
 for a in ${LATE_AGES:-0 8 7 9}; do
     run late$a GOSSIP_LATE_AGE=$a
 done
+timeout -k 10 600 python -u -m pytest tests/test_late_exit_gpu.py -x -v --timeout 300 --timeout-method thread -m gpu > gpurun_out/gpu_late.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/gpu_late.log; [ $rc -eq 0 ] || exit 1
