@@ -267,7 +267,8 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *                      (callers then split the shares into more shards)   [GOSSIP_MEM_LIMIT]
  *   "late_age"         k_pull stops gathering a node's peer rows of a tile at least this many
  *                      ticks old once they cover every bit it can still take (bottom-up early
- *                      exit); 0 = off                                         [GOSSIP_LATE_AGE]
+ *                      exit); 0 = off, -1 = auto (1: every tile of a CSR pull; 0 in DENSE
+ *                      mode, which gathers nothing)                          [GOSSIP_LATE_AGE]
  *   "xchunks"          row partition: row chunks per tick of the pipelined exchange, 1..16 (4);
  *                      equal on every rank of a partition                    [GOSSIP_XCHUNKS] */
 int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value);
@@ -335,6 +336,8 @@ typedef struct gossip_counters {
      * young_overlap option is on), HIP events on the engine stream (TIMING) */
     double pull_phase_ms;
     uint64_t young_line2_misses; /* second slot lines fetched without a hint (k_pull_young) */
+    uint32_t pull_late_age;      /* late_age in effect for the last pull (0: no early exit) */
+    uint32_t pad0;
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 int gossip_engine_reset_timing(gossip_engine* e);

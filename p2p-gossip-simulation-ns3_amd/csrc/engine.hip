@@ -446,6 +446,11 @@ struct YoungPack {
 
 constexpr int kRing = 4;   // host staging slots
 constexpr int kLag = 2;    // ticks of lag before liveness is read back
+// late_age auto: the exit test on every tile.  A tile whose frontier rows are sparse never
+// exits (its unseen bits are not covered before the last peer), and the test costs a few
+// shuffles per peer batch: C4 1.179e13 -> 1.259e13 edge events/s (peer rows 274 -> 216 GB per
+// launch, ages 7/8 alone give the same), C3 3.11 -> 3.07 ms per tick (profiles/r02/late_ab.txt)
+constexpr int64_t kAutoLateAge = 1;
 constexpr uint32_t kTileWords = 16;  // allocation unit: 16 words = 1024 shares = 128 B per row
 // second-line hint stamp of tick t (young_kernel.h): never 0, the value hint bytes start with
 inline uint32_t hint_stamp(int64_t t) { return 1u + (uint32_t)(((t % 255) + 255) % 255); }
@@ -572,7 +577,10 @@ struct gossip_engine {
     int64_t opt_young_grid = 0;       // k_pull_young blocks, 0 = the pull grid
     int64_t opt_pull_gate = 1;        // k_pull: occupancy-gated own-seen loads
     int64_t opt_young_waves = 4;      // k_pull_young register budget: waves per SIMD (4, 5, 6)
-    int64_t opt_late_age = 0;         // k_pull early exit for tiles >= this many ticks old (0: off)
+    int64_t opt_late_age = -1;        // k_pull early exit for tiles >= this many ticks old (0: off, -1: auto)
+    int64_t late_age_now() const {    // auto: every tile of a gathering (CSR) pull
+        return opt_late_age >= 0 ? opt_late_age : dense ? 0 : kAutoLateAge;
+    }
     hipStream_t ystream = nullptr;    // the second stream (created on first use)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers_phase;  // pull phase (both kernels)
@@ -1425,10 +1433,10 @@ int gossip_engine::tick_step_a(int64_t t) {
                           (c.keep != ~0ull ? WF_KEEP : 0u) | (c.snap ? WF_SNAP : 0u));
         keep_any |= c.keep != ~0ull;
     }
-    if (opt_late_age > 0)  // bottom-up early exit in k_pull for tiles at least late_age ticks old
+    if (const int64_t late = late_age_now())  // bottom-up early exit in k_pull (tiles >= late ticks old)
         for (uint32_t w = 0; w < hw; w++) {
             const uint32_t tl = w / kTileWords;
-            if (tile_alloc[tl] && t + 1 - tile_first[tl] >= opt_late_age) WF[w] |= (uint8_t)WF_LATE;
+            if (tile_alloc[tl] && t + 1 - tile_first[tl] >= late) WF[w] |= (uint8_t)WF_LATE;
         }
     for (uint32_t i = 0; i < ny; i++)  // k_pull leaves these words to k_pull_young
         if (YP->yt[i].flags)
@@ -2098,7 +2106,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_young_waves = env_option("GOSSIP_YOUNG_WAVES", 4);
         e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
         e->opt_xchunks = env_option("GOSSIP_XCHUNKS", 4);
-        e->opt_late_age = env_option("GOSSIP_LATE_AGE", 0);
+        e->opt_late_age = env_option("GOSSIP_LATE_AGE", -1);
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
         e->dense = cfg->mode == GOSSIP_MODE_DENSE;
         e->handshake = (cfg->flags & GOSSIP_F_HANDSHAKE) != 0;
@@ -2378,7 +2386,7 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
         if (e->have_sched) return set_error(GOSSIP_ESTATE, "mem_limit: set before the schedule");
         e->opt_mem_limit = value;
     } else if (k == "late_age") {
-        if (value < 0 || value > 1000) return set_error(GOSSIP_EINVAL, "late_age: 0 (off) .. 1000 ticks");
+        if (value < -1 || value > 1000) return set_error(GOSSIP_EINVAL, "late_age: -1 (auto), 0 (off) .. 1000 ticks");
         e->opt_late_age = value;
     } else if (k == "xchunks") {
         if (value < 1 || value > (int64_t)gossip_engine::kMaxChunks) return set_error(GOSSIP_EINVAL, "xchunks: 1 .. 16 row chunks");
@@ -2816,6 +2824,7 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     // 5 B per peer (id + second-line hint), 8 B per own seen word, row_ptr + counters per node
     // and launch
     c->young_line2_misses = acct[15];
+    c->pull_late_age = (uint32_t)e->late_age_now();
     c->young_bytes_moved = 128ull * (acct[8] + acct[10] + acct[13] + acct[14] + acct[15]) + 5ull * acct[9] +
                            8ull * (acct[11] + acct[12]) + e->young_launches * (8ull * (e->n + 1) + 16ull * e->n);
     uint64_t g = 0;

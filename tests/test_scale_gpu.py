@@ -155,7 +155,7 @@ def test_c4_sample_matches_oracle_a(gossip, oracle, c4):
         ("nt rows, 3-block grid", (("pull_nt", 1), ("pull_grid", 3))),
         ("64 word-lanes", (("pull_lpw", 64),)),
         ("every live seen pair read (no occupancy gate)", (("pull_gate", 0),)),
-        ("bottom-up early exit on every tile", (("late_age", 1),)),
+        ("no bottom-up early exit (late_age 0; the default exits on every tile)", (("late_age", 0),)),
         ("bottom-up early exit on tiles >= 4 ticks old, nt rows", (("late_age", 4), ("pull_nt", 1))),
     ]
     for name, opts in variants:
