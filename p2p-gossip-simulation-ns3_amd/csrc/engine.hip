@@ -451,6 +451,7 @@ constexpr int kLag = 2;    // ticks of lag before liveness is read back
 // shuffles per peer batch: C4 1.179e13 -> 1.259e13 edge events/s (peer rows 274 -> 216 GB per
 // launch, ages 7/8 alone give the same), C3 3.11 -> 3.07 ms per tick (profiles/r02/late_ab.txt)
 constexpr int64_t kAutoLateAge = 1;
+constexpr double kYoungMinEntries = 16.0;  // young auto: expected slot entries per node (see alloc_device)
 constexpr uint32_t kTileWords = 16;  // allocation unit: 16 words = 1024 shares = 128 B per row
 // second-line hint stamp of tick t (young_kernel.h): never 0, the value hint bytes start with
 inline uint32_t hint_stamp(int64_t t) { return 1u + (uint32_t)(((t % 255) + 255) % 255); }
@@ -895,7 +896,13 @@ int gossip_engine::alloc_device() {
         if (opt_young == 1 && !ok)
             return set_error(GOSSIP_EINVAL, "young tiles need the CSR tick engine (not DENSE, HOP_BATCH, "
                                             "HANDSHAKE, NOSKIP or a row partition)");
-        young = ok && (opt_young == 1 || (opt_young == -1 && n >= (1u << 20)));
+        // auto: the frontier rows outgrow the caches (n >= 2^20) and the young tiles hold enough
+        // bits to pay for their per-node slot reads: expected slot entries per node, ~ births per
+        // tick x deg^(young_age - 1) / n, >= kYoungMinEntries (C4 at 2 / 4 shards: ~50 / ~25
+        // entries, young tiles win; at 8 shards ~12: they lose 8 %, profiles/r02/)
+        const double avg_deg = n ? (double)nnz / n : 0.0;
+        const double est_entries = (double)max_births * std::pow(avg_deg, (double)(opt_young_age - 1)) / std::max<uint32_t>(n, 1);
+        young = ok && (opt_young == 1 || (opt_young == -1 && n >= (1u << 20) && est_entries >= kYoungMinEntries));
     }
     // slots, plus the second-line hints (young_kernel.h): reverse-edge index + 2 hint bytes per entry
     const uint64_t slot_bytes = young ? 2ull * n * kSlotU16 * 2u + nnz * 6u : 0ull;

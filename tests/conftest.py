@@ -15,12 +15,26 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP engine)")
 
 
+def _stale(target, srcs):
+    # missing, or a source edited after the build (60 s of slack: a copied tree whose files all
+    # got one extraction time is not "stale")
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(f) > t + 60 for f in srcs if os.path.exists(f))
+
+
 def _ensure_built():
-    libs = [os.path.join(ROOT, "oracle", "liboracle.so"), os.path.join(PKG, "lib", "libgossip.so")]
-    if all(os.path.exists(p) for p in libs):
-        return
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-    subprocess.run(["make", "-s", "-C", os.path.join(PKG, "csrc")], check=True)
+    # a libgossip.so older than its sources is rebuilt, never tested; a fresh tree is left alone
+    csrc = os.path.join(PKG, "csrc")
+    srcs = [os.path.join(csrc, f) for f in os.listdir(csrc)] + [os.path.join(ROOT, "include", "gossip.h")]
+    odir = os.path.join(ROOT, "oracle")
+    osrcs = [os.path.join(odir, f) for f in ("oracle.cpp", "oracle_b.cpp", "oracle.h", "Makefile")]
+    for d, target, ss in ((odir, os.path.join(odir, "liboracle.so"), osrcs),
+                          (csrc, os.path.join(PKG, "lib", "libgossip.so"), srcs)):
+        if _stale(target, ss):
+            print(f"conftest: {target} missing or older than its sources, rebuilding", file=sys.stderr)
+            subprocess.run(["make", "-s", "-C", d], check=True)
 
 
 _ensure_built()

@@ -146,11 +146,11 @@ def test_c4_sample_matches_oracle_a(gossip, oracle, c4):
     del a, b
     assert ref.edge_events > 10_000_000 and int((ref.gen + ref.recv - ref.processed).sum()) >= 1
     variants = [
-        ("auto (young-tile slots on at 10M nodes)", ()),
-        ("young tiles off", (("young", 0),)),
-        ("young tiles, 8-entry slots (overflow paths at scale)", (("young_cap", 8),)),
-        ("young tiles after k_pull on one stream", (("young_overlap", 0),)),
-        ("young tiles concurrent, k_pull launched first", (("young_overlap", 2),)),
+        ("auto (this 11-generation sample is too thin for young tiles)", ()),
+        ("young-tile slots forced on", (("young", 1),)),
+        ("young tiles, 8-entry slots (overflow paths at scale)", (("young", 1), ("young_cap", 8))),
+        ("young tiles after k_pull on one stream", (("young", 1), ("young_overlap", 0))),
+        ("young tiles concurrent, k_pull launched first", (("young", 1), ("young_overlap", 2))),
         ("nt rows, 16384-block grid (the C4 production kernel)", (("pull_nt", 1), ("pull_grid", 16384))),
         ("nt rows, 3-block grid", (("pull_nt", 1), ("pull_grid", 3))),
         ("64 word-lanes", (("pull_lpw", 64),)),
@@ -198,6 +198,8 @@ def test_c4_bench_slice_invariants(gossip, c4):
     # later generations of ids whose earlier flood already covered the node: counted, not processed
     assert int((st.gen.astype(np.int64) + st.recv - st.processed).sum()) > 0
     assert c.words_hw > 500 and int(st.recv.sum()) > 100 * len(gens)
+    # the production pull: young-tile slots chosen automatically, the early exit on every tile
+    assert c.young_launches > 0 and c.pull_late_age == 1
 
 
 # ------------------------------------------------------------------------------------------- C5
