@@ -1641,29 +1641,34 @@ int gossip_engine::tick_step_a(int64_t t) {
         };
         if (nchunks > 1) {
             // Pipelined exchange: pull (+ the MFMA contraction) and births per row chunk, each
-            // chunk closed by its event so that its exchange overlaps the next chunk.  The pull
-            // timer then spans the whole chunked compute of the tick, births included.
+            // chunk closed by its event so that its exchange overlaps the next chunk.  Timed as
+            // without chunks: the MFMA contraction (DENSE) or the pull (CSR), summed over chunks.
+            const bool timing = (cfg.flags & GOSSIP_F_TIMING) != 0;
             for (uint32_t c = 0; c < nchunks; c++) {
                 uint64_t lo, hi;
                 chunk_rows(row_rank, c, &lo, &hi);
-                if (hi > lo) {
+                if (hi > lo) {  // (chunk 0 never is empty: a rank owns >= 512 rows)
+                    hipEvent_t c0 = timing ? (c ? get_event() : e0) : nullptr;
+                    hipEvent_t c1 = timing ? (c ? get_event() : e1) : nullptr;
+                    if (timing) HIP_TRY(hipEventRecord(c0, stream));
                     PullArgs ac = a;
                     ac.v0 = (uint32_t)lo;
                     ac.n = (uint32_t)hi;
                     if (dense) {
                         const int rc = run_dense(lo, hi);
                         if (rc) return rc;
+                        if (timing) HIP_TRY(hipEventRecord(c1, stream));
                         ac.inc = d_inc;
+                        run_pull(ac, false);
+                    } else {
+                        run_pull(ac, true);
+                        if (timing) HIP_TRY(hipEventRecord(c1, stream));
                     }
-                    run_pull(ac, !dense);
+                    if (timing) timers.emplace_back(c0, c1);
                 }
                 int rc = launch_births(cb_off[c], cb_off[c + 1] - cb_off[c]);
                 if (rc) return rc;
                 if ((rc = end_chunk(c))) return rc;
-            }
-            if (cfg.flags & GOSSIP_F_TIMING) {
-                HIP_TRY(hipEventRecord(e1, stream));
-                timers.emplace_back(e0, e1);
             }
         } else if (dense) {
             // The timed kernel in DENSE mode is the MFMA contraction; its incoming words are
