@@ -108,6 +108,29 @@ def cpu_baseline(topo, ev, sample_shares, hops):
                        f"(host nproc {os.cpu_count()}, threads=1)")
 
 
+def cpu_baseline_bitsliced(topo, ev, sample_shares, hops, threads):
+    """ORACLE B (bit-sliced, level-synchronous, multithreaded CPU restatement; SURVEY 8(d)'s
+    optional all-cores baseline, reported beside the single-core ORACLE A one): the first
+    `sample_shares` generations of the slice (distinct ids), floods cut after `hops` hops; the
+    timer covers the propagation, not the CSR construction."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    a, b = topo.links()
+    sub = ev[:sample_shares]
+    sub = sub[np.unique(sub["share_id"], return_index=True)[1]]  # distinct ids (ORACLE B's domain)
+    sub = sub[np.lexsort((sub["node"], sub["ns"]))]
+    t_cut = int(sub["ns"].max()) + hops * L_NS + 1
+    r = oracle.run_oracle_b(topo.num_nodes, L_NS, t_cut, a, b, sub["ns"], sub["node"], sub["share_id"],
+                            threads=threads)
+    return dict(value=r.edge_events / r.wall_s if r.wall_s > 0 else None, unit="edge events/s",
+                cores=threads, kind="port",
+                sample=f"ORACLE B (bit-sliced 64 shares per word, level-synchronous, {threads} threads) "
+                       f"on the same graph, the first {len(sub)} generations after t=10 s, floods "
+                       f"cut after {hops} hops: {r.edge_events} edge events in {r.wall_s:.2f} s of "
+                       f"propagation (host nproc {os.cpu_count()})")
+
+
 def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, flags):
     """Warm up and time every shard this rank owns; raises gossip.GossipError on failure."""
     W, K = args.warmup, args.steps
@@ -421,6 +444,12 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(topo, win, args.cpu_sample, args.cpu_hops)
             except Exception as e:  # the baseline is reported, never required
                 out["cpu_baseline"] = {"value": None, "error": str(e)}
+            try:
+                win = ev[ev["ns"] >= SLICE_NS]
+                out["cpu_baseline_bitsliced"] = cpu_baseline_bitsliced(topo, win, 64, args.cpu_hops,
+                                                                       args.threads)
+            except Exception as e:
+                out["cpu_baseline_bitsliced"] = {"value": None, "error": str(e)}
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -63,6 +63,7 @@ def load():
         lib.oracle_b_run.argtypes = [C.c_uint32, C.c_int64, C.c_int64, C.c_uint64, P, P, C.c_uint64,
                                      P, P, P, C.c_int] + [P] * 8
         lib.oracle_b_last_error.restype = C.c_char_p
+        lib.oracle_b_last_wall_s.restype = C.c_double
         _lib = lib
     return _lib
 
@@ -245,8 +246,9 @@ def run_oracle_b(num_nodes, latency_ns, t_cut_ns, link_a, link_b, ev_ns, ev_node
                           _vp(u[2]), _vp(sent), _vp(u[3]), _vp(u[4]), _vp(u[5]), C.byref(ee))
     if rc != 0:
         raise RuntimeError(lib.oracle_b_last_error().decode())
-    return OracleResult(u[0], u[1], u[2], sent, u[3], u[4], u[5], ee.value, 0, 0.0, (a, b),
-                        (ns, nd, ids), [], None)
+    # wall_s: the bit-sliced propagation only (CSR construction excluded)
+    return OracleResult(u[0], u[1], u[2], sent, u[3], u[4], u[5], ee.value, int(ns.size),
+                        float(lib.oracle_b_last_wall_s()), (a, b), (ns, nd, ids), [], None)
 
 
 def seconds_to_ns(s):

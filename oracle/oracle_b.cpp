@@ -22,6 +22,7 @@
 //
 // Work: 64 shares per 64-bit word; per hop, inc[v] = OR over distinct peers u of F[u].
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdint>
 #include <cstring>
@@ -34,6 +35,7 @@
 namespace {
 
 thread_local std::string g_err_b;
+thread_local double g_wall_b = 0.0;  // seconds of the last run's level-synchronous propagation
 
 int fail_b(const std::string& m) {
     g_err_b = m;
@@ -60,6 +62,9 @@ void par_for(uint64_t n, int threads, F&& f) {
 extern "C" {
 
 const char* oracle_b_last_error(void) { return g_err_b.c_str(); }
+// wall time of the last oracle_b_run's propagation (the bit-sliced BFS levels), without the
+// CSR construction: what a timed CPU baseline of the hot path measures
+double oracle_b_last_wall_s(void) { return g_wall_b; }
 
 int oracle_b_run(uint32_t n, int64_t latency_ns, int64_t t_cut_ns, uint64_t num_links,
                  const uint32_t* la, const uint32_t* lb, uint64_t num_events, const int64_t* ev_ns,
@@ -136,6 +141,7 @@ int oracle_b_run(uint32_t n, int64_t latency_ns, int64_t t_cut_ns, uint64_t num_
         s[ev_node[k]] += deg[ev_node[k]];
     }
     std::vector<uint64_t> F(n), Fn(n), seen(n);
+    const auto w0 = std::chrono::steady_clock::now();
     for (size_t b0 = 0; b0 < live_ev.size(); b0 += 64) {
         const size_t nb = std::min<size_t>(64, live_ev.size() - b0);
         std::fill(F.begin(), F.end(), 0ull);
@@ -175,6 +181,7 @@ int oracle_b_run(uint32_t n, int64_t latency_ns, int64_t t_cut_ns, uint64_t num_
             if (!any.load()) break;
         }
     }
+    g_wall_b = std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
     uint64_t ee = 0;
     for (uint32_t v = 0; v < n; v++) ee += s[v];
     if (gen) std::memcpy(gen, g.data(), n * 4ull);
