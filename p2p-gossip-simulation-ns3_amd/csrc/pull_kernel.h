@@ -32,7 +32,8 @@
 //                 nz_cur is clear) is not read: young tiles are mostly empty rows;
 //   covered    -- once the peer rows read so far hold every bit the node can still take
 //                 (live last tick, unseen, kept) in all words of a tile, the tile's remaining
-//                 peer rows cannot change `new` and are not read (bottom-up early exit);
+//                 peer rows cannot change `new` and are not read (bottom-up early exit, for
+//                 tiles flagged WF_LATE: every tile by default, option late_age);
 //   F_next tile rows are written only when some word of the tile got a bit (and the tile's
 //   occupancy bit set); rows left unwritten hold stale bits that no reader ever loads.
 #pragma once
@@ -51,15 +52,9 @@ enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u, WF_Y
 
 constexpr uint32_t kPullLdsWords = 2048;  // words per launch: LDS liveness, new liveness, flags
 #ifndef PULL_INFLIGHT
-#define PULL_INFLIGHT 8  // A/B builds: make variants (q4, q16)
+#define PULL_INFLIGHT 8  // A/B builds: make variants (q4, q12, q16)
 #endif
 constexpr int kInflight = PULL_INFLIGHT;  // peer-row loads in flight per lane
-#ifndef PULL_EARLY_EXIT
-// Opt-in (make variants -> libgossip_ee.so): on C4 it read 10% fewer peer-row bytes in the same
-// time, on C3 7% fewer bytes in 7% MORE time -- the exit test makes the next batch of peer
-// loads wait for the previous batch (profiles/r01/early_exit_ab.json).
-#define PULL_EARLY_EXIT 0
-#endif
 // Non-temporal row accesses: a template switch of k_pull<LPW,1>, chosen at launch by bitmap size
 // (engine.hip, kPullNtBytes).  On C4 (97 GB bitmaps) every row access non-temporal ran 128.6 ms
 // per launch against 132.1 ms; on C3 (2 GB bitmaps) 3.59 ms against 3.31 ms
@@ -292,7 +287,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                         // the <= 8 occupancy bits of this pass's tiles, tested per lane by tile
                         const uint32_t nzp = (uint32_t)(nzw >> ((((w - 2u * wl) >> 4)) & 63u)) & 0xffu;
                         for (int t0 = 0; t0 < rem; t0 += kInflight) {
-                            int open = (a.noskip || !(PULL_EARLY_EXIT || late))
+                            int open = (a.noskip || !late)
                                            ? 1 : (((want0 & ~acc0) | (want1 & ~acc1)) != 0ull);
                             open |= __shfl_xor(open, 1, GRP);  // per tile (8 word-lanes)
                             open |= __shfl_xor(open, 2, GRP);
