@@ -23,9 +23,10 @@
 // product; C/D: lane l, register g -> row (g&3) + 8(g>>2) + 4(l>>5), column l&31.
 //
 // Tiling: block = 8 waves (2 x 4), output tile 256 rows x 256 columns (4 frontier words), wave
-// tile 128 x 64 = 4 x 2 MFMA tiles (128 accumulator registers).  K advances 512 (64 B of bits
-// per row) per stage through double-buffered LDS (2 x 40 KB, rows padded to 80 B: 5r mod 16 is a
-// permutation, so 16 lanes' ds_read_b128 hit distinct 16-B slots).  One barrier per stage: the
+// tile 128 x 64 = 4 x 2 MFMA tiles (128 accumulator registers).  K advances kStageK = 1024 (128 B
+// of bits per row) per stage through double-buffered LDS (2 x 72 KB, rows padded to 144 B: 9r mod
+// 16 is a permutation, so 16 lanes' ds_read_b128 hit distinct 16-B slots; 512-k stages with 80-B
+// rows measured 3 % lower MFMA utilisation, twice the barriers).  One barrier per stage: the
 // stage's bit loads are issued a stage ahead.  A stage whose frontier bits are all zero for the
 // block's 256 columns is skipped (__syncthreads_or), so sparse frontiers cost only the loads.
 // Blocks are mapped XCD-major: the 4 column tiles of one row block run on one XCD together, so
@@ -46,10 +47,15 @@ struct BitsArgs {
     uint32_t mb0;                    // first row block (row partition)
 };
 
-constexpr uint32_t kDenseTile = 256;   // rows / columns per block tile
-constexpr uint32_t kStageK = 512;      // k per LDS stage
-constexpr uint32_t kStageRow = 80;     // padded LDS row: 64 B of bits + 16
-constexpr uint32_t kDensePad = 512;    // n_pad multiple (tile and stage)
+#ifndef DENSE_STAGE_K
+#define DENSE_STAGE_K 1024  // 512: 0.478 / 0.554 MFMA util on C2 / C5, 1024: 0.494 / 0.568 (half the barriers; profiles/r02/dense_stage_ab.txt)
+#endif
+constexpr uint32_t kDenseTile = 256;               // rows / columns per block tile
+constexpr uint32_t kStageK = DENSE_STAGE_K;        // k per LDS stage
+constexpr uint32_t kStageQ = kStageK / 128u;       // 16-B pieces of a row per stage
+constexpr uint32_t kStageRow = kStageK / 8u + 16u; // padded LDS row: the stage's bits + 16 B
+constexpr uint32_t kDensePad = kStageK;            // n_pad multiple (tile and stage)
+static_assert(kStageK % 512u == 0u && ((kStageRow / 16u) & 1u), "stage: odd 16-B row pitch");
 
 // Frontier bitmap (node rows of share words) -> one bit row per share column.  A wave takes
 // 64 nodes x one word and transposes the 64 x 64 bit block with ballots.
@@ -114,9 +120,10 @@ __global__ __launch_bounds__(512, 1) void k_dense_bits(BitsArgs a) {
     const uint32_t op = t >> 8, lrow = t & 255u;
     const uint32_t* src = op == 0 ? a.Ab + (uint64_t)(mblk * kDenseTile + lrow) * a.kw
                                   : a.FT + (uint64_t)(nt * kDenseTile + lrow) * a.kw;
-    uint4 r[4];
+    uint4 r[kStageQ];
 #pragma unroll
-    for (int q = 0; q < 4; q++) r[q] = *reinterpret_cast<const uint4*>(src + (uint64_t)sb * 16u + 4u * q);
+    for (uint32_t q = 0; q < kStageQ; q++)
+        r[q] = *reinterpret_cast<const uint4*>(src + (uint64_t)sb * (kStageK / 32u) + 4u * q);
 
     const uint32_t h = lane >> 5, rr = lane & 31u;
     uint32_t msk[4];
@@ -133,24 +140,25 @@ __global__ __launch_bounds__(512, 1) void k_dense_bits(BitsArgs a) {
         const uint32_t p = (s - sb) & 1u;
         uint8_t* wr = &S[p][op][lrow * kStageRow];
 #pragma unroll
-        for (int q = 0; q < 4; q++) *reinterpret_cast<uint4*>(wr + 16 * q) = r[q];
+        for (uint32_t q = 0; q < kStageQ; q++) *reinterpret_cast<uint4*>(wr + 16u * q) = r[q];
         int bnz = 0;
         if (op == 1) {
-            const uint4 o = make_uint4(r[0].x | r[1].x | r[2].x | r[3].x, r[0].y | r[1].y | r[2].y | r[3].y,
-                                       r[0].z | r[1].z | r[2].z | r[3].z, r[0].w | r[1].w | r[2].w | r[3].w);
-            bnz = (o.x | o.y | o.z | o.w) != 0u;
+            uint32_t o = 0u;
+#pragma unroll
+            for (uint32_t q = 0; q < kStageQ; q++) o |= r[q].x | r[q].y | r[q].z | r[q].w;
+            bnz = o != 0u;
         }
         if (s + 1u < se) {
 #pragma unroll
-            for (int q = 0; q < 4; q++)
-                r[q] = *reinterpret_cast<const uint4*>(src + (uint64_t)(s + 1u) * 16u + 4u * q);
+            for (uint32_t q = 0; q < kStageQ; q++)
+                r[q] = *reinterpret_cast<const uint4*>(src + (uint64_t)(s + 1u) * (kStageK / 32u) + 4u * q);
         }
         if (!__syncthreads_or(bnz)) continue;  // no frontier bit in this k range: nothing to add
         computed++;
         const uint8_t* As = &S[p][0][0];
         const uint8_t* Bs = &S[p][1][0];
 #pragma unroll
-        for (uint32_t kq = 0; kq < 4; kq++) {  // 128 k = 16 B of each row
+        for (uint32_t kq = 0; kq < kStageQ; kq++) {  // 128 k = 16 B of each row
             uint4 xa[4], xb[2];
 #pragma unroll
             for (int i = 0; i < 4; i++)
