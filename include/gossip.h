@@ -65,6 +65,12 @@ int gossip_topology_create(uint32_t num_nodes, double connection_prob, uint32_t 
 /* Import an explicit key list (e.g. a dump of an NS-3 run); keys are (a,b), a != b. */
 int gossip_topology_from_links(uint32_t num_nodes, uint64_t num_links, const uint32_t* a,
                                const uint32_t* b, gossip_topology** out);
+/* Read a key list written by gossip_sim --dumpLinks: one "a b" pair of unsigned decimals per line
+ * (spaces or tabs, blank lines skipped).  Strict: a missing or extra field, a sign, a non-digit,
+ * an overflow, a node >= num_nodes or a self-loop is GOSSIP_EINVAL naming the line (the
+ * reference's own parser, Share::FromString p2pnode.cc:13-30, leaves fields uninitialised on
+ * malformed input).  Then as gossip_topology_from_links. */
+int gossip_topology_load_links(uint32_t num_nodes, const char* path, gossip_topology** out);
 uint32_t gossip_topology_num_nodes(const gossip_topology* t);
 uint64_t gossip_topology_num_links(const gossip_topology* t);
 /* Keys in std::map order. */
@@ -99,8 +105,12 @@ typedef struct gossip_schedule gossip_schedule;
 int gossip_schedule_create(uint32_t num_nodes, uint32_t node_seed, int64_t t_start_ns,
                            int64_t t_cut_ns, int64_t t_gen_end_ns, uint32_t id_mask,
                            int num_threads, gossip_schedule** out);
+/* Events in any order (sorted here); a negative ns is GOSSIP_EINVAL. */
 int gossip_schedule_from_events(uint64_t num_events, const gossip_gen_event* ev,
                                 gossip_schedule** out);
+/* Read events written by gossip_sim --dumpEvents: "ns node shareId" per line, parsed as strictly
+ * as gossip_topology_load_links (ns <= INT64_MAX, node < num_nodes unless num_nodes is 0). */
+int gossip_schedule_load_events(uint32_t num_nodes, const char* path, gossip_schedule** out);
 /* Synthetic schedule generated on GPU `device` (schedule_gpu.hip): the reference's rules --
  * first event at U(2,5) s, then every U(2,5) s; counted iff t_start <= t < t_cut (and
  * < t_gen_end if nonzero); shareId from GenerateUniqueShareId's formula -- with each node's
@@ -196,6 +206,14 @@ int gossip_engine_add_snapshot(gossip_engine* e, int64_t t_ns);
 int gossip_engine_set_row_partition(gossip_engine* e, uint32_t rank, uint32_t count);
 int gossip_rccl_unique_id(uint8_t* out, uint32_t len); /* len >= 128 (ncclUniqueId) */
 int gossip_engine_connect_rccl(gossip_engine* e, const uint8_t* unique_id, uint32_t len);
+/* Abort the engine's RCCL communicator (ncclCommAbort).  The one call that may be made from
+ * another thread while the engine is inside gossip_engine_run: when one rank of a partition
+ * fails, its peers are blocked in a collective that can never complete; aborting their
+ * communicators makes their gossip_engine_run return GOSSIP_EHIP instead of hanging.  A no-op
+ * without a communicator; the engine is then only good for gossip_engine_destroy. */
+int gossip_engine_abort(gossip_engine* e);
+/* Lockstep backend: the ranks' engines must all be on ONE device (the unpack reads the other
+ * ranks' messages in place; no peer access is enabled). */
 int gossip_engine_group_run(gossip_engine** engines, uint32_t count, int64_t tick_end);
 /* The exchange moves only OCCUPIED 16-word tile rows of F_next (the tile-occupancy bits), with
  * the occupancy words, per-node row offsets and the rank's liveness words: one message per rank

@@ -215,3 +215,138 @@ __global__ __launch_bounds__(512, 1) void k_dense_bits(BitsArgs a) {
     if (lo && v < a.n) atomicOr(ip, (unsigned long long)lo);
     if (hi && v + 64u < a.n) atomicOr(ip + 64ull * a.stride, (unsigned long long)hi);
 }
+
+// ------------------------------------------------------------------------------------------
+// k_dense_dedup -- the rest of the DENSE-mode pull after the contraction: for every node and
+// live word, new = inc & ~seen & keep (+ group_fix), seen |= new, F_next = new, recv/sent +=
+// popcount(new) (p2pnode.cc:155-165, 189), tile occupancy and liveness -- the same per-pair
+// semantics as k_pull's incoming-word path, but laid out for the chip rather than for a gather:
+// one node per wave step (lane = a 16-B word pair of a 128-word pass), the grid's waves striding
+// over the engine's rows.  k_pull serves 64 nodes per wave because its peer-id / occupancy
+// pipeline is per 64-node chunk; with nothing to gather that layout left a 4,096-node graph
+// 64 waves for the whole chip (C2: 307 us per dispatch).  HBM-bound: per live pair 16 B of
+// incoming words read (+ zeroed when non-zero), 16 B of seen read and written, 16 B of F_next
+// written.  Liveness: per block an LDS OR, then one global atomicOr per word only when the
+// block adds bits the word does not already hold (most blocks add none).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_dense_dedup(PullArgs a) {
+    extern __shared__ unsigned long long smem[];
+    unsigned long long* s_lp = smem;
+    unsigned long long* s_new = smem + a.wact;
+    uint8_t* s_wf = reinterpret_cast<uint8_t*>(smem + 2u * a.wact);
+    unsigned long long* s_keep = smem + 2u * a.wact + ((a.wact + 15u) & ~15u) / 8u;
+    for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
+        const uint8_t f = a.wflags[a.wbase + i];
+        s_lp[i] = (a.live_prev && !a.noskip) ? a.live_prev[a.wbase + i] : ~0ull;
+        s_new[i] = 0ull;
+        s_wf[i] = f;
+        if (a.keep_lds) s_keep[i] = (f & WF_KEEP) ? a.ctl[a.wbase + i].keep : ~0ull;
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t stride = a.stride;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint32_t npass = (a.wact + 127u) / 128u;
+    unsigned long long snap_local = 0ull;
+    uint32_t t_srd = 0, t_swr = 0, t_fwr = 0;  // wave-uniform traffic accounting
+    for (uint64_t v = a.v0 + wave; v < a.n; v += nwaves) {
+        uint32_t cnt = 0;
+        unsigned long long nzacc = 0ull;
+        for (uint32_t pass = 0; pass < npass; pass++) {
+            const uint32_t lw = pass * 128u + 2u * lane;
+            const uint32_t w = a.wbase + lw;
+            const bool act = lw < a.wact;
+            uint32_t f0 = 0, f1 = 0;
+            uint64_t lp0 = 0ull, lp1 = 0ull;
+            if (act) {
+                const uint16_t fl = *reinterpret_cast<const uint16_t*>(s_wf + lw);
+                f0 = fl & 0xffu;
+                f1 = fl >> 8;
+                lp0 = s_lp[lw];
+                lp1 = s_lp[lw + 1u];
+            }
+            const bool dead = (lp0 | lp1) == 0ull;
+            ulonglong2 s2 = make_ulonglong2(0ull, 0ull), x = make_ulonglong2(0ull, 0ull);
+            ulonglong2* ip = reinterpret_cast<ulonglong2*>(a.inc + v * stride + w);
+            if (act && !dead) {  // the two loads of the pair, in flight together
+                s2 = *reinterpret_cast<const ulonglong2*>(a.seen + v * stride + w);
+                x = *ip;
+            }
+            if (f0 & WF_CLEAR) s2.x = 0ull;
+            if (f1 & WF_CLEAR) s2.y = 0ull;
+            uint64_t k0 = ~0ull, k1 = ~0ull;
+            if (act && (f0 & WF_KEEP)) k0 = s_keep[lw];
+            if (act && (f1 & WF_KEEP)) k1 = s_keep[lw + 1u];
+            uint64_t n0 = 0ull, n1 = 0ull;
+            if (act && !dead) {
+                if ((x.x | x.y) != 0ull) *ip = make_ulonglong2(0ull, 0ull);  // consumed
+                n0 = x.x & ~s2.x & k0;
+                n1 = x.y & ~s2.y & k1;
+                if (f0 & WF_GROUP) n0 = group_fix(n0, s2.x, a.ctl[w].gmask, a.ctl[w].gstart);
+                if (f1 & WF_GROUP) n1 = group_fix(n1, s2.y, a.ctl[w + 1].gmask, a.ctl[w + 1].gstart);
+            }
+            // a 16-word tile row of F_next is written (and marked occupied) iff it got a bit
+            int ta = (n0 | n1) != 0ull || (a.noskip && act);
+            ta |= __shfl_xor(ta, 1, 64);
+            ta |= __shfl_xor(ta, 2, 64);
+            ta |= __shfl_xor(ta, 4, 64);
+            const bool swr = act && (dead ? ((f0 | f1) & WF_CLEAR) != 0u
+                                          : ((n0 | n1) != 0ull || ((f0 | f1) & WF_CLEAR) != 0u));
+            t_fwr += wave_count(act && ta);
+            t_srd += wave_count(act && !dead);
+            t_swr += wave_count(swr);
+            if (act) {
+                uint64_t* sp = a.seen + v * stride + w;
+                if (ta) *reinterpret_cast<ulonglong2*>(a.Fnext + v * stride + w) = make_ulonglong2(n0, n1);
+                if (swr) {
+                    if (dead && !((f0 & f1) & WF_CLEAR))
+                        sp[(f0 & WF_CLEAR) ? 0 : 1] = 0ull;
+                    else
+                        *reinterpret_cast<ulonglong2*>(sp) = make_ulonglong2(s2.x | n0, s2.y | n1);
+                }
+                if (!dead) {
+                    cnt += (uint32_t)(__popcll(n0) + __popcll(n1));
+                    if (a.snap) {
+                        if (f0 & WF_SNAP) snap_local += (unsigned long long)__popcll(n0 & a.ctl[w].snap);
+                        if (f1 & WF_SNAP) snap_local += (unsigned long long)__popcll(n1 & a.ctl[w + 1].snap);
+                    }
+                    if (n0) atomicOr(&s_new[lw], (unsigned long long)n0);
+                    if (n1) atomicOr(&s_new[lw + 1u], (unsigned long long)n1);
+                }
+            }
+            // occupancy word of the node: 8 tile bits per pass, written whole once per word
+            const uint32_t tw = (a.wbase + pass * 128u) >> 10;
+            unsigned long long nb = (ta && act && (lane & 7u) == 0u) ? 1ull << ((w >> 4) & 63u) : 0ull;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) nb |= __shfl_xor(nb, off, 64);
+            nzacc |= nb;
+            if (pass + 1u == npass || ((a.wbase + (pass + 1u) * 128u) >> 10) != tw) {
+                if (lane == 0) a.nz_next[v * a.ntw + tw] = nzacc;
+                nzacc = 0ull;
+            }
+        }
+        const uint32_t c = (uint32_t)wave_sum((unsigned long long)cnt);
+        if (lane == 0 && c) {
+            a.recv[v] += c;
+            a.sent[v] += (uint64_t)c * a.deg[v];
+        }
+    }
+    if (a.snap) {
+        snap_local = wave_sum(snap_local);
+        if (lane == 0 && snap_local) atomicAdd(a.snap, snap_local);
+    }
+    if (a.acct && lane == 0) {
+        const uint32_t tv[3] = {t_srd, t_swr, t_fwr};
+#pragma unroll
+        for (int q = 0; q < 3; q++)
+            if (tv[q]) atomicAdd(&a.acct[2 + q], (unsigned long long)tv[q]);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
+        const unsigned long long x = s_new[i];
+        if (!x) continue;
+        const unsigned long long have = __hip_atomic_load(&a.live[a.wbase + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (x & ~have) atomicOr(&a.live[a.wbase + i], x);
+    }
+}

@@ -27,6 +27,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -638,6 +639,7 @@ struct gossip_engine {
     uint64_t recv_cap = 0;
     uint64_t* d_sizes = nullptr;
     uint64_t sizes_cap = 0;
+    std::atomic<bool> aborted{false};  // gossip_engine_abort: comm torn down by another thread
     uint64_t exchange_bytes_out = 0, exchange_bytes_in = 0;
     bool tick_open = false;          // host-staged stepping: tick_begin done, tick_end pending
     // Pipelined exchange (option xchunks, row partition only): the own rows go through the pull
@@ -686,7 +688,7 @@ gossip_engine::~gossip_engine() {
         hipEventDestroy(p.first);
         hipEventDestroy(p.second);
     }
-    if (comm) ncclCommDestroy(comm);
+    if (comm && !aborted.load()) ncclCommDestroy(comm);  // (an aborted communicator is already freed)
     for (int k = 0; k < kRing; k++) {
         hipFree(d_ctl[k]); hipFree(d_births[k]); hipFree(d_gphase[k]); hipFree(d_wflags[k]);
         hipHostFree(h_wflags[k]);
@@ -1551,6 +1553,10 @@ int gossip_engine::tick_step_a(int64_t t) {
         };
         hipEvent_t e0 = nullptr, e1 = nullptr, p0 = nullptr, p1 = nullptr;
         a.inc = nullptr;
+        if (dense && (cfg.flags & GOSSIP_F_TIMING)) {  // DENSE phase: transpose + MFMA + dedup
+            p0 = get_event();
+            HIP_TRY(hipEventRecord(p0, stream));
+        }
         if (dense) {  // transpose the frontier to share-column bit rows (not timed as the pull)
             dim3 eg(n_pad / 256u, wact);
             k_transpose<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad / 32u, wact, a.live_prev,
@@ -1621,6 +1627,18 @@ int gossip_engine::tick_step_a(int64_t t) {
             young_launches++;
             return GOSSIP_OK;
         };
+        // DENSE mode: dedup of the incoming words of rows [base.v0, base.n), one node per wave
+        // step, the grid sized to the rows (k_dense_dedup, dense_kernel.h)
+        auto run_dedup = [&](const PullArgs& base) {
+            const uint64_t rows = base.n > base.v0 ? base.n - base.v0 : 0;
+            const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((rows + 3) / 4, 4096));
+            for (uint32_t wb = 0; wb < wact; wb += kPullLdsWords) {
+                PullArgs c = base;
+                c.wbase = wb;
+                c.wact = std::min(kPullLdsWords, wact - wb);
+                k_dense_dedup<<<g, 256, pull_lds_bytes(c.wact, c.keep_lds != 0), stream>>>(c);
+            }
+        };
         // the MFMA contraction of rows [lo, hi) (DENSE mode) into the incoming words
         auto run_dense = [&](uint64_t lo, uint64_t hi) -> int {
             BitsArgs gm;
@@ -1659,7 +1677,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                         if (rc) return rc;
                         if (timing) HIP_TRY(hipEventRecord(c1, stream));
                         ac.inc = d_inc;
-                        run_pull(ac, false);
+                        run_dedup(ac);
                     } else {
                         run_pull(ac, true);
                         if (timing) HIP_TRY(hipEventRecord(c1, stream));
@@ -1671,8 +1689,9 @@ int gossip_engine::tick_step_a(int64_t t) {
                 if ((rc = end_chunk(c))) return rc;
             }
         } else if (dense) {
-            // The timed kernel in DENSE mode is the MFMA contraction; its incoming words are
-            // then consumed by k_pull (dedup/state/counters, untimed).
+            // The timed kernel in DENSE mode is the MFMA contraction (pull_ms); its incoming
+            // words are then consumed by k_dense_dedup.  The whole phase -- transpose, MFMA,
+            // dedup -- is timed as pull_phase_ms.
             const int rc = run_dense(v0, v1);
             if (rc) return rc;
             if (cfg.flags & GOSSIP_F_TIMING) {
@@ -1680,7 +1699,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 timers.emplace_back(e0, e1);
             }
             a.inc = d_inc;
-            run_pull(a, false);
+            run_dedup(a);
         } else {
             if (overlap) {
                 HIP_TRY(hipEventRecord(ev_fork, stream));
@@ -1711,6 +1730,11 @@ int gossip_engine::tick_step_a(int64_t t) {
                 HIP_TRY(hipEventRecord(p1, stream));
                 timers_phase.emplace_back(p0, p1);
             }
+        }
+        if (dense && p0) {
+            p1 = get_event();
+            HIP_TRY(hipEventRecord(p1, stream));
+            timers_phase.emplace_back(p0, p1);
         }
         HIP_TRY(hipGetLastError());
         pull_launches++;
@@ -2283,6 +2307,13 @@ int gossip_rccl_unique_id(uint8_t* out, uint32_t len) {
     return GOSSIP_OK;
 }
 
+int gossip_engine_abort(gossip_engine* e) {
+    if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    bool expected = false;
+    if (e->comm && e->aborted.compare_exchange_strong(expected, true)) ncclCommAbort(e->comm);
+    return GOSSIP_OK;
+}
+
 int gossip_engine_connect_rccl(gossip_engine* e, const uint8_t* id, uint32_t len) {
     if (!e || !id || len < sizeof(ncclUniqueId)) return set_error(GOSSIP_EINVAL, "bad argument");
     if (e->comm) return set_error(GOSSIP_ESTATE, "already connected");
@@ -2293,7 +2324,7 @@ int gossip_engine_connect_rccl(gossip_engine* e, const uint8_t* id, uint32_t len
     return GOSSIP_OK;
 }
 
-// One device (or peer-visible devices), one thread: the engines of one row partition step in
+// One device, one thread: the engines of one row partition step in
 // lockstep and exchange rows with device copies -- the rehearsal backend of the RCCL exchange.
 int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end) {
     if (!es || count == 0) return set_error(GOSSIP_EINVAL, "NULL argument");
@@ -2302,6 +2333,9 @@ int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end
         if (!e || !e->have_sched) return set_error(GOSSIP_ESTATE, "set graph and schedule first");
         if (e->row_count != count || e->row_rank != r) return set_error(GOSSIP_EINVAL, "engines must be ranks 0..count-1 of one partition");
         if (e->comm) return set_error(GOSSIP_EINVAL, "group run is the non-RCCL backend");
+        // the unpack kernels read the other ranks' messages in place: one device only
+        if (e->device != es[0]->device)
+            return set_error(GOSSIP_EINVAL, "group run: every engine must be on the same device (no peer access)");
     }
     gossip_engine* e0 = es[0];
     if (tick_end > e0->tick_end) tick_end = e0->tick_end;
@@ -2482,6 +2516,13 @@ static int import_message(gossip_engine* e, uint32_t rank, uint32_t chunk, const
         return set_error(GOSSIP_EINVAL, "exchange_import_chunk: chunk >= gossip_engine_exchange_chunks");
     HIP_TRY(hipSetDevice(e->device));
     if ((rc = e->ensure_dev(e->d_recv_msgs, e->recv_cap, std::max<uint64_t>(bytes / 8, 1)))) return rc;
+    // The unpack ORs liveness into d_live and writes F_next / nz_next rows that this tick's
+    // engine-stream work clears first (tick_step_a's memsets): order it after the chunk, even
+    // when the caller imports before exporting its own message.
+    {
+        const uint32_t after = chunk == gossip_engine::kWholeRows ? e->nchunks - 1u : chunk;
+        HIP_TRY(hipStreamWaitEvent(e->xstream, e->ev_chunk[after], 0));
+    }
     HIP_TRY(hipMemcpyAsync(e->d_recv_msgs, buf, bytes, hipMemcpyHostToDevice, e->xstream));
     if ((rc = e->unpack_rows(e->cur, rank, chunk, e->d_recv_msgs, bytes / 8, e->xstream))) return rc;
     HIP_TRY(hipStreamSynchronize(e->xstream));  // (the receive buffer is reused by the next import)

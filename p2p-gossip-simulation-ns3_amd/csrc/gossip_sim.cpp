@@ -16,6 +16,7 @@
 // rank per device, with the per-tick frontier exchange over RCCL (gossip_engine_connect_rccl).
 #include <cerrno>
 #include <chrono>
+#include <condition_variable>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -164,10 +165,45 @@ struct Part {
     std::string err;
 };
 
+// The ranks of a row partition (--layout=rows) fail together.  Each rank's set-up (device,
+// memory budget, graph, schedule) can fail on that rank alone; the ranks therefore meet here
+// before ncclCommInitRank, which would otherwise wait forever for a rank that has given up.  A
+// rank that fails later, inside the run, aborts the other ranks' communicators
+// (gossip_engine_abort), so that they leave their collectives with an error instead of hanging.
+struct RowGroup {
+    std::mutex m;
+    std::condition_variable cv;
+    uint32_t count = 0, arrived = 0;
+    bool failed = false;
+    std::vector<gossip_engine*> live;  // engines that may be inside a collective (guarded by m)
+
+    // Every rank calls this exactly once, with its set-up status; true = all ranks are ready.
+    bool ready(uint32_t rank, gossip_engine* e, bool ok) {
+        std::unique_lock<std::mutex> lk(m);
+        if (!ok) failed = true;
+        else live[rank] = e;
+        arrived++;
+        cv.notify_all();
+        cv.wait(lk, [&] { return arrived == count; });
+        if (failed) live[rank] = nullptr;
+        return !failed;
+    }
+    // Rank `rank` failed (or finished): take its engine out, and on failure abort the others.
+    void leave(uint32_t rank, bool failure) {
+        std::lock_guard<std::mutex> lk(m);
+        live[rank] = nullptr;
+        if (!failure) return;
+        failed = true;
+        for (gossip_engine* e : live)
+            if (e) gossip_engine_abort(e);
+    }
+};
+
 // One engine, start to finish: shard `rank` of `count` (share sharding) or row rank `rank` of
-// `count` (layout rows, exchange over RCCL with the shared communicator id `uid`).
+// `count` (layout rows, exchange over RCCL with the shared communicator id `uid`; `group` is the
+// partition's rendezvous).
 void run_engine(const gossip_config& base, int device, bool rows, uint32_t rank, uint32_t count,
-                const uint8_t* uid, const gossip_topology* topo, const gossip_schedule* sched,
+                const uint8_t* uid, RowGroup* group, const gossip_topology* topo, const gossip_schedule* sched,
                 const std::vector<double>& per_t, bool link_timing, bool want_trace, double mem_limit_mb,
                 Part& out) {
     gossip_config cfg = base;
@@ -177,9 +213,12 @@ void run_engine(const gossip_config& base, int device, bool rows, uint32_t rank,
         cfg.shard_count = count;
     }
     gossip_engine* eng = nullptr;
+    bool met = group == nullptr;  // a row rank has passed the rendezvous
     auto fail = [&](const char* what, int rc) {
         out.rc = rc;
         out.err = std::string(what) + ": " + gossip_last_error();
+        if (!met) group->ready(rank, nullptr, false);  // (never leave the other ranks waiting)
+        else if (group) group->leave(rank, true);
         if (eng) gossip_engine_destroy(eng);
     };
     int rc = gossip_engine_create(&cfg, &eng);
@@ -194,11 +233,21 @@ void run_engine(const gossip_config& base, int device, bool rows, uint32_t rank,
     for (double t : per_t)  // Start(): p2pnetwork.cc:201-204
         if ((rc = gossip_engine_add_snapshot(eng, gossip_seconds_to_ns(t)))) return fail("snapshot", rc);
     if ((rc = gossip_engine_set_schedule_obj(eng, sched))) return fail("engine schedule", rc);
-    if (rows && count > 1 && (rc = gossip_engine_connect_rccl(eng, uid, 128))) return fail("rccl connect", rc);
+    if (group) {
+        met = true;
+        if (!group->ready(rank, eng, true)) {
+            out.rc = GOSSIP_ESTATE;
+            out.err = "another row rank failed during set-up";
+            gossip_engine_destroy(eng);
+            return;
+        }
+        if ((rc = gossip_engine_connect_rccl(eng, uid, 128))) return fail("rccl connect", rc);
+    }
     out.first_tick = gossip_engine_first_tick(eng);
     out.end_tick = gossip_engine_end_tick(eng);
     if ((rc = gossip_engine_run(eng, gossip_engine_end_tick(eng)))) return fail("engine run", rc);
     if ((rc = gossip_engine_sync(eng))) return fail("engine sync", rc);
+    if (group) group->leave(rank, false);  // (no collective after this point)
     const uint32_t n = base.num_nodes;
     out.gen.assign(n, 0); out.recv.assign(n, 0); out.fwd.assign(n, 0); out.proc.assign(n, 0);
     out.peers.assign(n, 0); out.sock.assign(n, 0); out.sent.assign(n, 0);
@@ -241,13 +290,7 @@ int main(int argc, char** argv) {
     // ---- CreateRandomTopology (p2pnetwork.cc:62-96) ----
     gossip_topology* topo = nullptr;
     if (!o.linksIn.empty()) {
-        FILE* f = std::fopen(o.linksIn.c_str(), "r");
-        if (!f) { std::perror(o.linksIn.c_str()); return 1; }
-        std::vector<uint32_t> a, b;
-        unsigned x, y;
-        while (std::fscanf(f, "%u %u", &x, &y) == 2) { a.push_back(x); b.push_back(y); }
-        std::fclose(f);
-        if (gossip_topology_from_links(o.numNodes, a.size(), a.data(), b.data(), &topo)) return die("topology import");
+        if (gossip_topology_load_links(o.numNodes, o.linksIn.c_str(), &topo)) return die("topology import");
     } else {
         int kind = GOSSIP_TOPO_EXACT;
         if (o.topology == "skip" || (o.topology == "auto" && o.numNodes > 16384)) kind = GOSSIP_TOPO_SKIP;
@@ -260,14 +303,7 @@ int main(int argc, char** argv) {
     // ---- share schedule (P2PNode RNGs, p2pnode.cc:33-43, 91-125) ----
     gossip_schedule* sched = nullptr;
     if (!o.eventsIn.empty()) {
-        FILE* f = std::fopen(o.eventsIn.c_str(), "r");
-        if (!f) { std::perror(o.eventsIn.c_str()); return 1; }
-        std::vector<gossip_gen_event> ev;
-        long long ns;
-        unsigned node, id;
-        while (std::fscanf(f, "%lld %u %u", &ns, &node, &id) == 3) ev.push_back({ns, node, id});
-        std::fclose(f);
-        if (gossip_schedule_from_events(ev.size(), ev.data(), &sched)) return die("schedule import");
+        if (gossip_schedule_load_events(n, o.eventsIn.c_str(), &sched)) return die("schedule import");
     } else if (o.schedule == "philox") {  // synthetic: per-node Philox streams, generated on the GPU
         if (gossip_schedule_create_philox(n, o.nodeSeed, t_start, t_cut, 0, o.device, &sched))
             return die("philox schedule");
@@ -330,6 +366,10 @@ int main(int argc, char** argv) {
         parts.assign(count, Part{});
         std::vector<uint8_t> uid(128, 0);
         if (rows && count > 1 && gossip_rccl_unique_id(uid.data(), 128)) return die("rccl unique id");
+        RowGroup group;
+        group.count = count;
+        group.live.assign(count, nullptr);
+        RowGroup* gp = rows && count > 1 ? &group : nullptr;
         auto w0 = std::chrono::steady_clock::now();
         std::vector<std::thread> th;
         const uint32_t ng = (uint32_t)o.gpus;
@@ -337,15 +377,15 @@ int main(int argc, char** argv) {
             th.emplace_back([&, g] {
                 // device g runs shards g, g + N, ... (rows: exactly rank g)
                 for (uint32_t r = g; r < count; r += ng)
-                    run_engine(cfg, o.device + (int)g, rows, r, count, uid.data(), topo, sched, per_t,
+                    run_engine(cfg, o.device + (int)g, rows, r, count, uid.data(), gp, topo, sched, per_t,
                                o.linkTiming, want_trace, o.memLimitMB, parts[r]);
             });
         for (auto& t : th) t.join();
         wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
         int worst = 0;
         std::string err;
-        for (const Part& p : parts)
-            if (p.rc) { worst = p.rc; err = p.err; }
+        for (const Part& p : parts)  // (report a rank's own failure over the ranks it stopped)
+            if (p.rc && (!worst || err.rfind("another row rank", 0) == 0)) { worst = p.rc; err = p.err; }
         if (!worst) break;
         if (!rows && (worst == GOSSIP_ECAPACITY || worst == GOSSIP_ENOMEM) && count < 4096) {
             std::fprintf(stderr, "gossip_sim: %u share shard(s) do not fit (%s); retrying with %u\n", count,

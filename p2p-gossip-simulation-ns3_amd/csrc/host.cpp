@@ -12,7 +12,9 @@
 //   PrintPeriodicStats        p2pnetwork.cc:231-250
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <new>
 #include <random>
@@ -487,14 +489,130 @@ int gossip_schedule_create(uint32_t num_nodes, uint32_t node_seed, int64_t t_sta
 int gossip_schedule_from_events(uint64_t num_events, const gossip_gen_event* ev,
                                 gossip_schedule** out) {
     if (!out || (num_events && !ev)) return set_error(GOSSIP_EINVAL, "NULL argument");
+    *out = nullptr;
+    for (uint64_t k = 0; k < num_events; k++)  // (a negative ns would also overflow hi - lo below)
+        if (ev[k].ns < 0)
+            return set_error(GOSSIP_EINVAL, "generation event " + std::to_string(k) + " has a negative time");
     try {
         auto s = std::make_unique<gossip_schedule>();
         s->ev.assign(ev, ev + num_events);
-        sort_events(s->ev, 1);
+        int64_t lo = INT64_MAX, hi = 0;
+        for (const auto& e : s->ev) {
+            lo = std::min(lo, e.ns);
+            hi = std::max(hi, e.ns);
+        }
+        if (num_events && (uint64_t)((hi - lo) >> 20) > 4 * num_events + 1024)
+            std::sort(s->ev.begin(), s->ev.end(), [](const gossip_gen_event& a, const gossip_gen_event& b) {
+                return a.ns != b.ns ? a.ns < b.ns : a.node < b.node;
+            });  // a sparse span: the bucket sort's table would dwarf the events
+        else
+            sort_events(s->ev, 1);
         *out = s.release();
         return GOSSIP_OK;
     } catch (const std::bad_alloc&) {
         return set_error(GOSSIP_ENOMEM, "host allocation failed");
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Dump files (gossip_sim --dumpLinks / --dumpEvents), read strictly.  The reference parses its
+// messages with an unchecked getline/stoul chain (Share::FromString, p2pnode.cc:13-30) that
+// leaves fields uninitialised on malformed input; here every malformed line is GOSSIP_EINVAL.
+// ---------------------------------------------------------------------------------------
+static bool read_file(const char* path, std::string& text) {
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return false;
+    char buf[1 << 16];
+    size_t k;
+    while ((k = std::fread(buf, 1, sizeof buf, f)) > 0) text.append(buf, k);
+    const bool ok = !std::ferror(f);
+    std::fclose(f);
+    return ok;
+}
+
+// Splits `text` into lines of exactly `nf` unsigned decimal fields (<= max[i] each), separated
+// by spaces or tabs; blank lines are skipped, a trailing '\r' is allowed.  Calls row(fields) for
+// every line; returns "" or the error text naming the line.
+static std::string parse_rows(const std::string& text, int nf, const uint64_t* max,
+                              const std::function<std::string(const uint64_t*)>& row) {
+    uint64_t vals[4];
+    size_t pos = 0, line = 0;
+    while (pos < text.size()) {
+        size_t end = text.find('\n', pos);
+        if (end == std::string::npos) end = text.size();
+        line++;
+        size_t i = pos, stop = end;
+        if (stop > i && text[stop - 1] == '\r') stop--;
+        int got = 0;
+        for (;;) {
+            while (i < stop && (text[i] == ' ' || text[i] == '\t')) i++;
+            if (i >= stop) break;
+            if (got == nf) return "line " + std::to_string(line) + ": more than " + std::to_string(nf) + " fields";
+            uint64_t v = 0;
+            const size_t d0 = i;
+            while (i < stop && text[i] >= '0' && text[i] <= '9') {
+                const uint64_t dig = (uint64_t)(text[i] - '0');
+                if (v > (max[got] - dig) / 10) return "line " + std::to_string(line) + ": field " +
+                                                       std::to_string(got + 1) + " out of range";
+                v = v * 10 + dig;
+                i++;
+            }
+            if (i == d0 || (i < stop && text[i] != ' ' && text[i] != '\t'))
+                return "line " + std::to_string(line) + ": field " + std::to_string(got + 1) +
+                       " is not an unsigned decimal integer";
+            vals[got++] = v;
+        }
+        if (got != 0 && got != nf)
+            return "line " + std::to_string(line) + ": " + std::to_string(got) + " field(s), expected " +
+                   std::to_string(nf);
+        if (got) {
+            std::string e = row(vals);
+            if (!e.empty()) return "line " + std::to_string(line) + ": " + e;
+        }
+        pos = end + 1;
+    }
+    return "";
+}
+
+int gossip_topology_load_links(uint32_t num_nodes, const char* path, gossip_topology** out) {
+    if (!out || !path) return set_error(GOSSIP_EINVAL, "NULL argument");
+    *out = nullptr;
+    try {
+        std::string text;
+        if (!read_file(path, text)) return set_error(GOSSIP_EINVAL, std::string("cannot read ") + path);
+        std::vector<uint32_t> a, b;
+        const uint64_t mx[2] = {0xffffffffull, 0xffffffffull};
+        const std::string err = parse_rows(text, 2, mx, [&](const uint64_t* v) -> std::string {
+            if (v[0] >= num_nodes || v[1] >= num_nodes) return "node id beyond --numNodes";
+            if (v[0] == v[1]) return "self-loop";
+            a.push_back((uint32_t)v[0]);
+            b.push_back((uint32_t)v[1]);
+            return "";
+        });
+        if (!err.empty()) return set_error(GOSSIP_EINVAL, std::string(path) + ": " + err);
+        return gossip_topology_from_links(num_nodes, a.size(), a.data(), b.data(), out);
+    } catch (const std::bad_alloc&) {
+        return set_error(GOSSIP_ENOMEM, "host allocation failed reading links");
+    }
+}
+
+int gossip_schedule_load_events(uint32_t num_nodes, const char* path, gossip_schedule** out) {
+    if (!out || !path) return set_error(GOSSIP_EINVAL, "NULL argument");
+    *out = nullptr;
+    try {
+        std::string text;
+        if (!read_file(path, text)) return set_error(GOSSIP_EINVAL, std::string("cannot read ") + path);
+        std::vector<gossip_gen_event> ev;
+        const uint64_t mx[3] = {(uint64_t)INT64_MAX, 0xffffffffull, 0xffffffffull};
+        const std::string err = parse_rows(text, 3, mx, [&](const uint64_t* v) -> std::string {
+            if (num_nodes && v[1] >= num_nodes) return "node id beyond --numNodes";
+            ev.push_back(gossip_gen_event{(int64_t)v[0], (uint32_t)v[1], (uint32_t)v[2]});
+            return "";
+        });
+        if (!err.empty()) return set_error(GOSSIP_EINVAL, std::string(path) + ": " + err);
+        return gossip_schedule_from_events(ev.size(), ev.data(), out);
+    } catch (const std::bad_alloc&) {
+        return set_error(GOSSIP_ENOMEM, "host allocation failed reading events");
     }
 }
 

@@ -59,7 +59,8 @@ EXPORTED_SYMBOLS = (
     "gossip_engine_exchange_export", "gossip_engine_exchange_import", "gossip_engine_tick_end",
     "gossip_schedule_create_philox", "gossip_engine_exchange_chunks",
     "gossip_engine_exchange_export_chunk", "gossip_engine_exchange_import_chunk",
-    "gossip_format_netanim",
+    "gossip_format_netanim", "gossip_topology_load_links", "gossip_schedule_load_events",
+    "gossip_engine_abort",
 )
 
 # NS-3 5 Mbps point-to-point links (p2pnetwork.cc:113): ns per byte, PPP+IPv4+TCP(timestamp
@@ -134,6 +135,9 @@ def load_library(path: str = LIB_PATH):
         "gossip_milliseconds_to_ns": (i64, [C.c_double]),
         "gossip_topology_create": (C.c_int, [u32, C.c_double, u32, C.c_int, C.c_int, C.POINTER(P)]),
         "gossip_topology_from_links": (C.c_int, [u32, u64, P, P, C.POINTER(P)]),
+        "gossip_topology_load_links": (C.c_int, [u32, C.c_char_p, C.POINTER(P)]),
+        "gossip_schedule_load_events": (C.c_int, [u32, C.c_char_p, C.POINTER(P)]),
+        "gossip_engine_abort": (C.c_int, [P]),
         "gossip_topology_num_nodes": (u32, [P]),
         "gossip_topology_num_links": (u64, [P]),
         "gossip_topology_get_links": (C.c_int, [P, P, P]),
@@ -254,6 +258,15 @@ class Topology:
         _check(lib.gossip_topology_from_links(n, a.size, _vp(a), _vp(b), C.byref(h)), "topology")
         return cls(h.value)
 
+    @classmethod
+    def load_links(cls, n: int, path: str):
+        """A key list written by gossip_sim --dumpLinks, parsed strictly (GossipError, code
+        GOSSIP_EINVAL, naming the line of any malformed entry)."""
+        lib = load_library()
+        h = C.c_void_p()
+        _check(lib.gossip_topology_load_links(n, os.fsencode(path), C.byref(h)), "load links")
+        return cls(h.value)
+
     @property
     def num_nodes(self) -> int:
         return int(load_library().gossip_topology_num_nodes(self._h))
@@ -297,6 +310,22 @@ def make_schedule(n: int, node_seed: int, t_start_ns: int, t_cut_ns: int, t_gen_
     h = C.c_void_p()
     _check(lib.gossip_schedule_create(n, node_seed, t_start_ns, t_cut_ns, t_gen_end_ns, id_mask,
                                       threads, C.byref(h)), "schedule")
+    try:
+        m = int(lib.gossip_schedule_size(h))
+        ev = np.empty(m, GEN_EVENT_DTYPE)
+        if m:
+            _check(lib.gossip_schedule_get(h, _vp(ev)), "schedule get")
+        return ev
+    finally:
+        lib.gossip_schedule_destroy(h)
+
+
+def load_events(n: int, path: str) -> np.ndarray:
+    """Generation events written by gossip_sim --dumpEvents ("ns node shareId" per line), parsed
+    strictly like Topology.load_links; sorted by (ns, node)."""
+    lib = load_library()
+    h = C.c_void_p()
+    _check(lib.gossip_schedule_load_events(n, os.fsencode(path), C.byref(h)), "load events")
     try:
         m = int(lib.gossip_schedule_size(h))
         ev = np.empty(m, GEN_EVENT_DTYPE)

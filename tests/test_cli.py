@@ -93,3 +93,15 @@ def test_cli_netanim_with_packets(gossip, oracle, tmp_path):
     r = oracle.run_reference(num_nodes=30, connection_prob=0.2, sim_time_s=12.0, topo_seed=5, node_seed=7)
     recs = P_RE.findall(xml)
     assert len(recs) == int(r.sent.sum()) > 0
+
+
+@pytest.mark.gpu
+def test_cli_rows_rank_failure_does_not_hang():
+    # --layout=rows, 2 ranks: on a 1-GPU box rank 1 cannot create its engine.  Rank 0 must not
+    # wait forever in ncclCommInitRank for it (the ranks meet before RCCL init and fail together).
+    p = subprocess.run([SIM, "--numNodes=3000", "--connectionProb=0.01", "--simTime=6", "--gpus=2",
+                        "--layout=rows", "--quiet"], capture_output=True, text=True, timeout=180)
+    if p.returncode == 0:  # a box with two visible GPUs ran the partition
+        assert "row ranks (RCCL exchange)" in p.stdout
+        return
+    assert "engine create" in p.stderr, p.stderr

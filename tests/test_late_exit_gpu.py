@@ -54,6 +54,7 @@ def test_late_exit_matches_oracle(gossip, oracle, late_age, young):
     ek, ok = np.lexsort((sid, node)), np.lexsort((ti, tn))
     assert np.array_equal(node[ek], tn[ok]) and np.array_equal(sid[ek], ti[ok])
     assert np.array_equal(tick[ek], tt[ok] // lat) and np.array_equal(hop[ek], th[ok])
+    assert np.array_equal(via[ek], tv[ok])  # ReceiveShare vs own generation (p2pnode.cc:115-120,155-165)
     eng.close()
 
 

@@ -94,11 +94,13 @@ def main():
                "ticks": cs[0].ticks, "edge_events": edge,
                "per_rank_mfma_ms_avg": ms, "per_rank_mfma_util": util,
                "per_rank_mfma_ms_max": max(ms),
-               "projected_edge_events_per_s": edge / (cs[0].ticks * max(ms) * 1e-3),
+               # NOT a throughput: an upper bound from the slowest rank's MFMA kernel alone
+               "mfma_kernel_only_bound_excl_exchange_and_dedup": edge / (cs[0].ticks * max(ms) * 1e-3),
                "exchange_bytes_per_tick_per_rank": (n_ - n_ // R) * cs[0].words_hw * 8,
                "group_wall_s_serialised": wall,
-               "note": "projection = per-tick time of the slowest rank's MFMA kernel; the exchange "
-                       "(all-gather of the frontier rows) and the dedup pull are not in it"}
+               "note": "the bound uses only the per-tick time of the slowest rank's MFMA kernel: the "
+                       "exchange (all-gather of the frontier rows) and the dedup are not in it, so it "
+                       "is not an edge-event rate and must not be quoted as one"}
         print(json.dumps(out), flush=True)
         return
     ref = None
