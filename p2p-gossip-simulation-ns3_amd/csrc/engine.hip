@@ -535,7 +535,9 @@ struct gossip_engine {
     std::vector<Snap> snaps;
     // ---- device state
     uint64_t* d_F[2] = {nullptr, nullptr};
-    uint64_t* d_seen = nullptr;
+    uint64_t* d_seen = nullptr;      // row v's seen words at d_seen + v * stride (v in [seen_lo, seen_lo + seen_n))
+    uint64_t* d_seen_mem = nullptr;  // the allocation: a row-partitioned rank holds only its own rows
+    uint32_t seen_lo = 0, seen_n = 0;
     // CSR mode: tile occupancy of F[0]/F[1] (n x ntw words, bit per 16-word tile row)
     unsigned long long* d_nz[2] = {nullptr, nullptr};
     uint32_t ntw = 0;
@@ -677,7 +679,7 @@ gossip_engine::~gossip_engine() {
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
     hipFree(d_rowptr_c); hipFree(d_col_c); hipFree(d_degc);
     for (int k = 0; k < 4; k++) { hipFree(d_smask[k]); hipHostFree(h_smask[k]); }
-    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
+    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen_mem); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     hipFree(d_msg); hipFree(d_cnt); hipFree(d_scan_tmp); hipFree(d_recv_msgs); hipFree(d_sizes);
@@ -931,7 +933,12 @@ int gossip_engine::alloc_device() {
         stride = (uint32_t)std::max<uint64_t>(stride, std::min<uint64_t>(want / kTileWords * kTileWords, fit));
     }
     const uint64_t bm = (uint64_t)n * stride * 8;
-    const uint64_t need = 3 * bm + (uint64_t)n * 24 + (nnz * 4) + ((uint64_t)n + 1) * 8 + slot_bytes +
+    // seen rows: a row-partitioned rank dedups only its own rows (F_cur / F_next stay whole: the
+    // pull reads every peer's row, the exchange writes the other ranks' rows)
+    seen_lo = row_count > 1 ? v0 : 0u;
+    seen_n = row_count > 1 ? v1 - v0 : n;
+    const uint64_t bm_seen = (uint64_t)seen_n * stride * 8;
+    const uint64_t need = 2 * bm + bm_seen + (uint64_t)n * 24 + (nnz * 4) + ((uint64_t)n + 1) * 8 + slot_bytes +
                           (dense ? (uint64_t)stride * 8 * n_pad : 0ull);
     if (need > (uint64_t)freeb)
         return set_error(GOSSIP_ENOMEM, "device memory: need " + std::to_string(need) +
@@ -939,10 +946,11 @@ int gossip_engine::alloc_device() {
                                             "-word window, " + std::to_string(freeb) + " free");
     HIP_TRY(hipMalloc(&d_F[0], bm));
     HIP_TRY(hipMalloc(&d_F[1], bm));
-    HIP_TRY(hipMalloc(&d_seen, bm));
+    HIP_TRY(hipMalloc(&d_seen_mem, std::max<uint64_t>(bm_seen, 8)));
+    d_seen = d_seen_mem - (uint64_t)seen_lo * stride;
     HIP_TRY(hipMemsetAsync(d_F[0], 0, bm, stream));
     HIP_TRY(hipMemsetAsync(d_F[1], 0, bm, stream));
-    HIP_TRY(hipMemsetAsync(d_seen, 0, bm, stream));
+    HIP_TRY(hipMemsetAsync(d_seen_mem, 0, bm_seen, stream));
     {
         ntw = (stride + 1023u) / 1024u;
         const size_t nzb = (size_t)n * ntw * 8;
@@ -1022,7 +1030,7 @@ int gossip_engine::alloc_device() {
         HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&live_done[k], hipEventDisableTiming));
     }
-    device_bytes = 3 * bm + 16ull * n * ntw + (uint64_t)n * 20 + nnz * 4 + ((uint64_t)n + 1) * 8 + 2ull * stride * 8 + slot_bytes +
+    device_bytes = 2 * bm + bm_seen + 16ull * n * ntw + (uint64_t)n * 20 + nnz * 4 + ((uint64_t)n + 1) * 8 + 2ull * stride * 8 + slot_bytes +
                    kRing * ((uint64_t)stride * sizeof(WordCtl) + (uint64_t)bcap * sizeof(Birth) + pcap * 4);
     if (dense) {
         const uint64_t ft = (uint64_t)stride * 8 * n_pad;
@@ -1074,17 +1082,20 @@ int gossip_engine::grow(uint32_t new_stride) {
         return set_error(GOSSIP_ECAPACITY, "live-share window exceeded " + std::to_string(stride) +
                                                " words per node and there is no device memory to widen it" +
                                                (comm ? " (on some rank of the row partition)" : ""));
-    uint64_t** bufs[3] = {&d_F[0], &d_F[1], &d_seen};
+    uint64_t** bufs[3] = {&d_F[0], &d_F[1], &d_seen_mem};
     for (uint64_t** b : bufs) {
+        const uint64_t rows = *b == d_seen_mem ? seen_n : n;
         uint64_t* nbuf = nullptr;
-        HIP_TRY(hipMalloc(&nbuf, nb));
-        HIP_TRY(hipMemsetAsync(nbuf, 0, nb, stream));
-        HIP_TRY(hipMemcpy2DAsync(nbuf, (size_t)new_stride * 8, *b, (size_t)stride * 8, (size_t)stride * 8, n,
-                                 hipMemcpyDeviceToDevice, stream));
+        HIP_TRY(hipMalloc(&nbuf, std::max<uint64_t>(rows * new_stride * 8, 8)));
+        HIP_TRY(hipMemsetAsync(nbuf, 0, rows * new_stride * 8, stream));
+        if (rows)
+            HIP_TRY(hipMemcpy2DAsync(nbuf, (size_t)new_stride * 8, *b, (size_t)stride * 8, (size_t)stride * 8, rows,
+                                     hipMemcpyDeviceToDevice, stream));
         HIP_TRY(hipStreamSynchronize(stream));
         HIP_TRY(hipFree(*b));
         *b = nbuf;
     }
+    d_seen = d_seen_mem - (uint64_t)seen_lo * new_stride;
     auto regrow_dev = [&](auto*& p, size_t elem, size_t oldn, size_t newn) -> int {
         void* q = nullptr;
         HIP_TRY(hipMalloc(&q, newn * elem));
@@ -1157,7 +1168,7 @@ int gossip_engine::grow(uint32_t new_stride) {
     word_insts.resize(new_stride);
     col_phase.resize((size_t)new_stride * 64, 0);
     col_src.resize((size_t)new_stride * 64, UINT32_MAX);
-    device_bytes += 3 * (nb - (uint64_t)n * stride * 8);
+    device_bytes += (2ull * n + seen_n) * (uint64_t)(new_stride - stride) * 8;
     stride = new_stride;
     grows++;
     return GOSSIP_OK;
@@ -2293,7 +2304,6 @@ int gossip_engine_set_row_partition(gossip_engine* e, uint32_t rank, uint32_t co
     if (e->have_graph) return set_error(GOSSIP_ESTATE, "set the row partition before the graph");
     if (count == 0 || rank >= count) return set_error(GOSSIP_EINVAL, "row partition: rank >= count");
     if (e->handshake) return set_error(GOSSIP_EINVAL, "row partition: not with GOSSIP_F_HANDSHAKE");
-    if (e->cfg.shard_count > 1) return set_error(GOSSIP_EINVAL, "row partition: not with share sharding");
     e->row_rank = rank;
     e->row_count = count;
     return GOSSIP_OK;

@@ -28,13 +28,22 @@ def _engine(gossip, topo, ev, lat, t_cut, opts, flags):
     return eng
 
 
-@pytest.mark.parametrize("late_age,young", [(1, 0), (3, 0), (4, 1), (2, 1)])
-def test_late_exit_matches_oracle(gossip, oracle, late_age, young):
+@pytest.fixture(scope="module")
+def late_case(gossip, oracle):
+    # one workload and ONE ORACLE A run (the costly part) for every variant below
     n = 6000
     topo = gossip.Topology.gnp(n, 16.0 / (n - 1), 91, gossip.TOPO_SKIP)
     lat = gossip.milliseconds_to_ns(5.0)
     t_cut = gossip.seconds_to_ns(7.37)  # a cut inside a tick: keep masks on late words
     ev = gossip.make_schedule(n, 92, T0, t_cut, id_mask=0x3FFF)  # id groups
+    a, b = topo.links()
+    r = oracle.run_replay(n, lat, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=True)
+    return topo, lat, t_cut, ev, r
+
+
+@pytest.mark.parametrize("late_age,young", [(1, 0), (3, 0), (4, 1), (2, 1)])
+def test_late_exit_matches_oracle(gossip, late_case, late_age, young):
+    topo, lat, t_cut, ev, r = late_case
     # a fresh tile per tick keeps the window wider than 64 words: the one-peer-walk-per-node
     # pull (k_pull<32, 1>) that carries the exit
     # (young tiles only up to age 2, so that k_pull still sees tiles with unseen bits)
@@ -45,8 +54,6 @@ def test_late_exit_matches_oracle(gossip, oracle, late_age, young):
     base = _engine(gossip, topo, ev, lat, t_cut, dict(yo, late_age=0), gossip.F_TILE_PER_TICK)
     assert eng.counters().pull_pair_edges < base.counters().pull_pair_edges  # the exit was taken
     base.close()
-    a, b = topo.links()
-    r = oracle.run_replay(n, lat, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=True)
     for k in STATS:
         assert np.array_equal(getattr(st, k), getattr(r, k)), (late_age, k)
     node, sid, tick, hop, via = eng.trace()

@@ -71,7 +71,9 @@ def test_group_run_matches_single_engine_and_oracle(gossip, oracle, mode, n, p, 
         parts = [e.snapshot(k) for e in ranks]
         assert all(x[0] == t_ns and x[1] == g_tot for x in parts)
         assert sum(x[2] for x in parts) == p_tot
-    if n <= 1500:  # (ORACLE A's event loop: seconds here, minutes on the larger graphs)
+    # ORACLE A on the sparse cases (seconds); the dense single engine is pinned to ORACLE A in
+    # test_engine_gpu.py (here its event loop would take ~30 s per case)
+    if n <= 1500 and mode == "csr":
         a, b = topo.links()
         r = oracle.run_replay(n, L, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
         for k in SUM:
@@ -125,3 +127,39 @@ def test_xchunks_mismatch_is_refused(gossip):
         ranks[0].set_option("xchunks", 17)
     for e in ranks:
         e.close()
+
+
+@pytest.mark.parametrize("mode,p", [("csr", 0.01), ("dense", 0.3)])
+def test_hybrid_share_shards_by_row_ranks(gossip, mode, p):
+    # S share shards x R row ranks (the layout a 10M-node row rank needs to fit one
+    # card): the ranks of each share shard run one row partition (lockstep backend); every rank
+    # holds only its own rows of seen.  The S x R engines' counters sum to the single engine's,
+    # with id collisions (groups stay inside one share shard).
+    n, S, R = 1600, 2, 3
+    topo = gossip.Topology.gnp(n, p, 61, gossip.TOPO_EXACT)
+    t_cut = gossip.seconds_to_ns(7.1)
+    ev = gossip.make_schedule(n, 62, T0, t_cut, id_mask=0x7FFF if mode == "csr" else 0)
+    m = gossip.MODE_DENSE if mode == "dense" else gossip.MODE_CSR
+    ref = _engine(gossip, n, t_cut, topo, ev, m, 0)
+    ref.run()
+    ref.sync()
+    want = ref.stats()
+    ref.close()
+    parts = []
+    for s in range(S):
+        ranks = []
+        for r in range(R):
+            e = gossip.Engine(n, L, T0, t_cut, mode=m, shard_rank=s, shard_count=S)
+            e.set_row_partition(r, R)
+            e.set_topology(topo)
+            e.set_schedule(ev)
+            ranks.append(e)
+        gossip.group_run(ranks)
+        for e in ranks:
+            e.sync()
+            parts.append(e.stats())
+            c = e.counters()
+            e.close()
+    for k in SUM:
+        total = sum(getattr(g, k).astype(np.uint64) for g in parts)
+        assert np.array_equal(total, getattr(want, k).astype(np.uint64)), k

@@ -137,29 +137,36 @@ def _c4_sample(gossip, c4):
 
 
 def test_c4_sample_matches_oracle_a(gossip, oracle, c4):
+    from concurrent.futures import ThreadPoolExecutor
+
     W = _w()
     topo = c4[0]
     n = topo.num_nodes
     ev, t_cut = _c4_sample(gossip, c4)
     a, b = topo.links()
-    ref = oracle.run_replay(n, W.L_NS, W.T0_NS, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
-    del a, b
-    assert ref.edge_events > 10_000_000 and int((ref.gen + ref.recv - ref.processed).sum()) >= 1
+    # ORACLE A (CPU, ~30 s at 10M nodes; the ctypes call releases the GIL) runs beside the GPU
+    # variants below
+    pool = ThreadPoolExecutor(1)
+    fut = pool.submit(oracle.run_replay, n, W.L_NS, W.T0_NS, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
+    # (the sample's window is <= 16 words: the pull is k_pull<8..16, 1>, whatever pull_lpw says)
     variants = [
         ("auto (this 11-generation sample is too thin for young tiles)", ()),
         ("young-tile slots forced on", (("young", 1),)),
         ("young tiles, 8-entry slots (overflow paths at scale)", (("young", 1), ("young_cap", 8))),
         ("young tiles after k_pull on one stream", (("young", 1), ("young_overlap", 0))),
-        ("young tiles concurrent, k_pull launched first", (("young", 1), ("young_overlap", 2))),
         ("nt rows, 16384-block grid (the C4 production kernel)", (("pull_nt", 1), ("pull_grid", 16384))),
         ("nt rows, 3-block grid", (("pull_nt", 1), ("pull_grid", 3))),
-        ("64 word-lanes", (("pull_lpw", 64),)),
         ("every live seen pair read (no occupancy gate)", (("pull_gate", 0),)),
         ("no bottom-up early exit (late_age 0; the default exits on every tile)", (("late_age", 0),)),
-        ("bottom-up early exit on tiles >= 4 ticks old, nt rows", (("late_age", 4), ("pull_nt", 1))),
     ]
+    runs = []
     for name, opts in variants:
-        st, c = _run(gossip, topo, ev, W.T0_NS, t_cut, options=opts, max_words=16)
+        runs.append((name, opts) + _run(gossip, topo, ev, W.T0_NS, t_cut, options=opts, max_words=16))
+    ref = fut.result()
+    pool.shutdown()
+    del a, b
+    assert ref.edge_events > 10_000_000 and int((ref.gen + ref.recv - ref.processed).sum()) >= 1
+    for name, opts, st, c in runs:
         _same(st, ref, what=name)
         if opts and opts[0] == ("pull_nt", 1):
             assert c.pull_nt == 1 and c.pull_grid == dict(opts)["pull_grid"]
@@ -170,36 +177,64 @@ def test_c4_sample_matches_oracle_a(gossip, oracle, c4):
         assert np.array_equal(tot[k], getattr(ref, k).astype(np.uint64)), ("2 shards", k)
 
 
-def test_c4_bench_slice_invariants(gossip, c4):
-    # The bench's workload: shard 0 of 2 of the C4 slice (every generation of the 16 ticks before
-    # t = 10 s and of the timed ticks, plus all earlier generations of their ids), 5 warm-up +
-    # 20 timed ticks, ~280 GiB of device memory.
+def _c4_shard_deltas(gossip, topo, ev, shard, shards, t0, t1):
+    W = _w()
+    eng = gossip.Engine(topo.num_nodes, W.L_NS, W.T0_NS, W.T_CUT_NS, shard_rank=shard, shard_count=shards)
+    eng.set_topology(topo)
+    eng.set_schedule(ev)
+    eng.run(t0)
+    eng.sync()
+    s0, c0 = eng.stats(), eng.counters()
+    eng.run(t1)
+    eng.sync()
+    s1, c1 = eng.stats(), eng.counters()
+    eng.close()
+    return s0, s1, c0, c1
+
+
+def test_c4_bench_slice_equals_continuous_run(gossip, c4):
+    # The bench's workload is the warm-start slice (every generation of the 16 ticks before
+    # t = 10 s and of the timed ticks, plus all earlier generations of their ids), ramped, then
+    # timed over ticks [2005, 2025).  Pinned here against the CONTINUOUS run (every generation
+    # from t = 5 s) of the same share shard: the per-node recv deltas and the edge events of the
+    # timed ticks must be identical (p2pnode.cc:189: an id's earlier floods are in the seen-sets
+    # either way).  Shard 0 of 4: the continuous run's start-up (the renewal density peaks ~7 s)
+    # needs ~25 % more live words than the steady state, more than half the shares fit one card.
     W = _w()
     topo = c4[0]
     n = topo.num_nodes
     warm, steps = 5, 20
-    t_end = W.SLICE_NS + (warm + steps + 1) * W.L_NS
-    ev, info = W.slice_schedule(n, W.CONFIGS["C4"]["node_seed"], W.SLICE_NS, t_end)
+    t0 = W.SLICE_NS // W.L_NS + warm
+    t1 = t0 + steps
+    ev_s, info = W.slice_schedule(n, W.CONFIGS["C4"]["node_seed"], W.SLICE_NS, t1 * W.L_NS)
     assert info["earlier_same_id"] > 0
-    owner = gossip.shard_events(topo, ev, 2)
-    eng = gossip.Engine(n, W.L_NS, W.T0_NS, W.T_CUT_NS, shard_rank=0, shard_count=2)
-    eng.set_topology(topo)
-    eng.set_schedule(ev)
-    tick_end = W.SLICE_NS // W.L_NS + warm + steps
-    eng.run(tick_end)
-    eng.sync()
-    st, c = eng.stats(), eng.counters()
-    eng.close()
-    _invariants(st, c)
-    mine = ev[owner == 0]
-    gens = mine[mine["ns"] < tick_end * W.L_NS]
-    assert int(st.gen.sum()) == len(gens) == c.generations
-    assert np.array_equal(st.gen, np.bincount(gens["node"], minlength=n).astype(np.uint32))
+    ev_c = gossip.make_schedule(n, W.CONFIGS["C4"]["node_seed"], W.T0_NS, W.T_CUT_NS, t_gen_end_ns=t1 * W.L_NS,
+                                threads=16)
+    shards = 4
+    own_s, own_c = gossip.shard_events(topo, ev_s, shards), gossip.shard_events(topo, ev_c, shards)
+    # the slice's events are a subset of the continuous run's, each on the same shard
+    key = lambda e: (e["ns"].astype(np.int64) << 24) | e["node"].astype(np.int64)  # noqa: E731 (ns < 2^34, n < 2^24)
+    sl_in_c = np.isin(key(ev_c), key(ev_s))
+    assert int(sl_in_c.sum()) == len(ev_s)
+    assert np.array_equal(own_c[sl_in_c], own_s)
+    a0, a1, ca0, ca1 = _c4_shard_deltas(gossip, topo, ev_s, 0, shards, t0, t1)
+    b0, b1, cb0, cb1 = _c4_shard_deltas(gossip, topo, ev_c, 0, shards, t0, t1)
+    for k in ("recv", "gen", "sent", "processed"):
+        da = getattr(a1, k).astype(np.int64) - getattr(a0, k).astype(np.int64)
+        db = getattr(b1, k).astype(np.int64) - getattr(b0, k).astype(np.int64)
+        assert np.array_equal(da, db), (k, int(np.count_nonzero(da != db)))
+    assert ca1.edge_events - ca0.edge_events == cb1.edge_events - cb0.edge_events > 0
+    # the slice run itself against the reference's counter invariants
+    _invariants(a1, ca1)
+    mine = ev_s[own_s == 0]
+    gens = mine[mine["ns"] < t1 * W.L_NS]
+    assert int(a1.gen.sum()) == len(gens) == ca1.generations
+    assert np.array_equal(a1.gen, np.bincount(gens["node"], minlength=n).astype(np.uint32))
     # later generations of ids whose earlier flood already covered the node: counted, not processed
-    assert int((st.gen.astype(np.int64) + st.recv - st.processed).sum()) > 0
-    assert c.words_hw > 500 and int(st.recv.sum()) > 100 * len(gens)
+    assert int((a1.gen.astype(np.int64) + a1.recv - a1.processed).sum()) > 0
+    assert ca1.words_hw > 200 and int(a1.recv.sum()) > 100 * len(gens)
     # the production pull: young-tile slots chosen automatically, the early exit on every tile
-    assert c.young_launches > 0 and c.pull_late_age == 1
+    assert ca1.young_launches > 0 and ca1.pull_late_age == 1
 
 
 # ------------------------------------------------------------------------------------------- C5
@@ -228,7 +263,7 @@ def test_c5_mfma_equals_csr_and_oracle_b(gossip, oracle, c5):
         _same(st, ref, what=f"C5 64 shares mode {mode} vs ORACLE B")
 
 
-@pytest.mark.parametrize("ranks", [2, 8])
+@pytest.mark.parametrize("ranks", [8])  # (2 ranks: tests/test_multiprocess_gpu.py, test_row_partition.py)
 def test_c5_row_partition_sums_to_single(gossip, c5, ranks):
     W = _w()
     topo, ev = c5

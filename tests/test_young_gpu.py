@@ -1,6 +1,7 @@
 """Young-tile slots (k_pull_young, young_kernel.h) against ORACLE A.
 
-Young tiles are switched on by default only for n >= 2^20 (C3/C4); here they are forced on small
+Young tiles are switched on by default only for n >= 2^20 (C4; C3's 1,000,000 nodes are just
+below); here they are forced on small
 graphs, with a fresh tile every tick (so every tick has young, leaving and fresh tiles), tiny slot
 capacities (so nodes overflow to dense rows, in the pull and in the births), every young age, and
 forced id collisions (id-group births that must find or cancel arrivals inside slots).  Per-node
@@ -91,12 +92,13 @@ def test_young_periodic_snapshots(gossip, oracle, monkeypatch):
     # PrintPeriodicStats partials counted inside k_pull_young (WF_SNAP) and k_births
     monkeypatch.setenv("GOSSIP_YOUNG", "1")
     monkeypatch.setenv("GOSSIP_YOUNG_CAP", "5")
-    sim = gossip.P2PGossipNetworkSimulation(2000, topo_seed=77, node_seed=78,
+    # (21 s: the snapshots at 10 s and 20 s, the second one inside the young-tile regime)
+    sim = gossip.P2PGossipNetworkSimulation(1200, topo_seed=77, node_seed=78,
                                             flags=gossip.F_TILE_PER_TICK)
-    sim.CreateRandomTopology(8.0 / 1999, 5.0)
-    st = sim.Start(31.0)
+    sim.CreateRandomTopology(8.0 / 1199, 5.0)
+    st = sim.Start(21.0)
     assert sim.engine.counters().young_launches > 0
-    ref = oracle.run_reference(num_nodes=2000, connection_prob=8.0 / 1999, sim_time_s=31.0,
+    ref = oracle.run_reference(num_nodes=1200, connection_prob=8.0 / 1199, sim_time_s=21.0,
                                topo_seed=77, node_seed=78)
     for k in STATS:
         assert np.array_equal(getattr(st, k), getattr(ref, k)), k

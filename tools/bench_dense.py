@@ -7,8 +7,10 @@ bit-sliced CSR pull (GOSSIP_MODE_CSR) on the same dense workload.  One JSON line
     python tools/bench_dense.py c5 --width 512 # C5 slice: 65,536 nodes, p=0.3, one flood batch
                                                # of `width` concurrent shares, 1 GPU
 
-MFMA utilisation = 2*M*N*K of the computed 128x128 output tiles / pull-kernel time / 5 POPS
-(the dense int8 peak: 2x the 2.5 PF dense bf16 rate, MI355X_MICROARCH.md "Matrix cores").
+MFMA utilisation = 2*M*N*K of the computed 128x128 output tiles / time / 5 POPS (the dense int8
+peak: 2x the 2.5 PF dense bf16 rate, MI355X_MICROARCH.md "Matrix cores"), over the MFMA kernel
+alone (mfma_util) and over the whole DENSE pull phase -- transpose + MFMA + dedup -- per dispatch
+(mfma_util_phase, phase_ms_avg).
 """
 import argparse
 import json
@@ -119,7 +121,15 @@ def main():
             out["dense_ops"] = c.dense_ops
             out["dense_tiles_skipped"] = c.dense_tiles_skipped
             out["mfma_tops"] = c.dense_ops / (c.pull_ms * 1e-3) / 1e12 if c.pull_ms else None
+            # kernel-only: k_dense_bits alone; phase: k_transpose + k_dense_bits + k_dense_dedup,
+            # HIP events around the three on the engine stream (the whole DENSE pull of a tick)
             out["mfma_util"] = c.dense_ops / (c.pull_ms * 1e-3) / INT8_PEAK_OPS if c.pull_ms else None
+            out["phase_ms_total"] = c.pull_phase_ms
+            out["phase_ms_avg"] = c.pull_phase_ms / max(c.pull_launches, 1)
+            out["mfma_util_phase"] = (c.dense_ops / (c.pull_phase_ms * 1e-3) / INT8_PEAK_OPS
+                                      if c.pull_phase_ms else None)
+            out["dedup_bytes_per_dispatch"] = 16 * (c.pull_seen_reads + c.pull_seen_writes + c.pull_f_writes) / max(
+                c.pull_launches, 1)
         else:
             out["pull_bytes_moved"] = c.pull_bytes_moved
             out["pull_tbs"] = c.pull_bytes_moved / (c.pull_ms * 1e-3) / 1e12 if c.pull_ms else None
