@@ -135,7 +135,7 @@ def test_hybrid_share_shards_by_row_ranks(gossip, mode, p):
     # card): the ranks of each share shard run one row partition (lockstep backend); every rank
     # holds only its own rows of seen.  The S x R engines' counters sum to the single engine's,
     # with id collisions (groups stay inside one share shard).
-    n, S, R = 1600, 2, 3
+    n, S, R = 2100, 2, 3  # (512-row blocks: ranks own 1024, 1024 and 52 rows)
     topo = gossip.Topology.gnp(n, p, 61, gossip.TOPO_EXACT)
     t_cut = gossip.seconds_to_ns(7.1)
     ev = gossip.make_schedule(n, 62, T0, t_cut, id_mask=0x7FFF if mode == "csr" else 0)
