@@ -195,6 +195,63 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
     return acc
 
 
+def rehearse_rows(args, wl, topo, ev, shards, R, flags):
+    """One GPU, share shard 0 of `shards`, run as the R row blocks of a row partition would run it
+    (engine option rehearse_rows; young tiles off, as on a row rank): per block and timed tick,
+    the pull over the block's rows, the pack of its F_next rows into its exchange message, the
+    unpack of that message (the work each OTHER rank does for it) and the message bytes.  A rank's
+    tick then costs its own pull + pack + the unpacks of the R - 1 other blocks, and it receives
+    the R - 1 other messages over xGMI.  Prints one JSON line marked REHEARSAL."""
+    W, K = args.warmup, args.steps
+    slice_tick = SLICE_NS // L_NS
+    eng = gossip.Engine(wl["nodes"], L_NS, T0_NS, T_CUT_NS, flags=flags, shard_rank=0, shard_count=shards)
+    try:
+        eng.set_option("young", 0)
+        eng.set_option("rehearse_rows", R)
+        eng.set_topology(topo)
+        eng.set_schedule(ev)
+        eng.run(slice_tick + W)
+        eng.sync()
+        eng.reset_timing()
+        c0 = eng.counters()
+        t0 = time.perf_counter()
+        eng.run(slice_tick + W + K)
+        eng.sync()
+        wall = time.perf_counter() - t0
+        c1 = eng.counters()
+        rh = eng.rehearsal(R)
+    finally:
+        eng.close()
+    T = max(rh["ticks"], 1)
+    pull, pack, unpack = rh["pull_ms"] / T, rh["pack_ms"] / T, rh["unpack_ms"] / T
+    msg = rh["msg_bytes"].astype(np.float64) / T
+    rank_ms = pull + pack + (unpack.sum() - unpack)  # own pull + own pack + the others' unpacks
+    ingress = msg.sum() - msg
+    n = wl["nodes"]
+    own_rows = np.diff(np.minimum(np.arange(R + 1) * (((n + R - 1) // R + 511) // 512 * 512), n))
+    fbytes = 2 * n * c1.words_cap * 8
+    out = {
+        "metric": "REHEARSAL: row partition, one rank's work per tick (not a throughput)",
+        "workload": f"{wl['desc']}, share shard 0 of {shards}, row blocks of an R = {R} partition, "
+                    f"{K} timed ticks after {W} warm-up from t = 10 s, young tiles off",
+        "rows_per_rank": own_rows.tolist(),
+        "edge_events_per_tick_whole_shard": (c1.edge_events - c0.edge_events) / T,
+        "pull_ms_per_tick": pull.tolist(),
+        "pack_ms_per_tick": pack.tolist(),
+        "unpack_ms_per_tick": unpack.tolist(),
+        "message_bytes_per_tick": msg.tolist(),
+        "rank_gpu_ms_per_tick": rank_ms.tolist(),
+        "rank_gpu_ms_per_tick_max": float(rank_ms.max()),
+        "rank_ingress_bytes_per_tick": ingress.tolist(),
+        "rank_ingress_bytes_per_tick_max": float(ingress.max()),
+        "unpartitioned_pull_ms_per_tick": c1.pull_ms / max(c1.pull_launches, 1),
+        "rank_device_gib": (fbytes + c1.words_cap * 8 * int(own_rows.max())) / 2**30,
+        "wall_s_rehearsal": wall,
+        "window_words": c1.words_hw,
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -212,12 +269,15 @@ def main():
     ap.add_argument("--rehearse-shards", type=int, default=0,
                     help="diagnostic: run only shard 0 of S on this one GPU (per-rank footprint "
                          "and time of an S-GPU run); the JSON line is marked REHEARSAL")
+    ap.add_argument("--rehearse-rows", type=int, default=0,
+                    help="diagnostic: one rank of an R-rank row partition of share shard 0 of "
+                         "--rehearse-shards (default: the workload's fit) on this one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    rehearsal = args.rehearse_shards > 1 and world == 1
+    rehearsal = (args.rehearse_shards > 1 or args.rehearse_rows > 1) and world == 1
     if args.gpus != world and not rehearsal:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N > 1 with "
                          f"torch.distributed.run (one process per GPU), or use --rehearse-shards")
@@ -261,6 +321,10 @@ def main():
             f"{len(ev)} generations in the slice schedule ({sinfo['earlier_same_id']} earlier "
             f"generations of recurring ids), setup {time.time() - t_setup:.1f} s")
 
+    if args.rehearse_rows > 1:
+        rehearse_rows(args, wl, topo, ev, max(args.rehearse_shards, wl["fit_shards"]), args.rehearse_rows,
+                      flags | gossip.F_TIMING)
+        return
     # Shards: at least what one GPU's HBM needs, at least one per rank, a multiple of the ranks;
     # doubled (on every rank) when any rank's engine runs out of device memory.
     passes = max(1, -(-wl["fit_shards"] // world))

@@ -288,7 +288,14 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *                      exit); 0 = off, -1 = auto (1: every tile of a CSR pull; 0 in DENSE
  *                      mode, which gathers nothing)                          [GOSSIP_LATE_AGE]
  *   "xchunks"          row partition: row chunks per tick of the pipelined exchange, 1..16 (4);
- *                      equal on every rank of a partition                    [GOSSIP_XCHUNKS] */
+ *                      equal on every rank of a partition                    [GOSSIP_XCHUNKS]
+ *   "rehearse_rows"    diagnostic, R >= 2 on an unpartitioned CSR engine (before the schedule;
+ *                      young tiles off, as on a row rank): the pull runs as R launches over the
+ *                      row blocks of an R-rank partition, and after each tick every block's
+ *                      F_next rows go through the exchange's pack and unpack kernels (unpacked
+ *                      into the same rows: results unchanged), each step timed per block with
+ *                      GOSSIP_F_TIMING -- one rank's compute and exchange work, measured on one
+ *                      GPU over the whole graph's data (gossip_engine_get_rehearsal) */
 int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value);
 /* The mode the engine runs (AUTO resolves at gossip_engine_set_graph). */
 int gossip_engine_mode(const gossip_engine* e);
@@ -358,6 +365,10 @@ typedef struct gossip_counters {
     uint32_t pad0;
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
+/* Option rehearse_rows = R: per row block r < R, summed since the last reset_timing -- pull time,
+ * pack time, unpack time (ms, HIP events) and message bytes; *ticks = ticks rehearsed. */
+int gossip_engine_get_rehearsal(gossip_engine* e, uint32_t ranges, double* pull_ms, double* pack_ms,
+                                double* unpack_ms, uint64_t* msg_bytes, uint64_t* ticks);
 int gossip_engine_reset_timing(gossip_engine* e);
 
 /* First-contact trace (GOSSIP_F_TRACE): one record per (node, shareId) whose first

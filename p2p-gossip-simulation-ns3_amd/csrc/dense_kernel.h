@@ -227,15 +227,19 @@ __global__ __launch_bounds__(512, 1) void k_dense_bits(BitsArgs a) {
 // 64 waves for the whole chip (C2: 307 us per dispatch).  HBM-bound: per live pair 16 B of
 // incoming words read (+ zeroed when non-zero), 16 B of seen read and written, 16 B of F_next
 // written.  Liveness: per block an LDS OR, then one global atomicOr per word only when the
-// block adds bits the word does not already hold (most blocks add none).
+// block adds bits the word does not already hold.  Blocks are 16 waves (1,024 threads) and
+// the grid at most 2 blocks per CU: the per-word liveness atomics of a launch scale with the
+// block count, and with 4-wave blocks (1,024 of them at C2) the same ~200 words took ~1,000
+// atomics each (134 us per dispatch).
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_dense_dedup(PullArgs a) {
+constexpr uint32_t kDedupWaves = 16;
+__global__ __launch_bounds__(1024) void k_dense_dedup(PullArgs a) {
     extern __shared__ unsigned long long smem[];
     unsigned long long* s_lp = smem;
     unsigned long long* s_new = smem + a.wact;
     uint8_t* s_wf = reinterpret_cast<uint8_t*>(smem + 2u * a.wact);
     unsigned long long* s_keep = smem + 2u * a.wact + ((a.wact + 15u) & ~15u) / 8u;
-    for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
+    for (uint32_t i = threadIdx.x; i < a.wact; i += blockDim.x) {
         const uint8_t f = a.wflags[a.wbase + i];
         s_lp[i] = (a.live_prev && !a.noskip) ? a.live_prev[a.wbase + i] : ~0ull;
         s_new[i] = 0ull;
@@ -245,8 +249,8 @@ __global__ __launch_bounds__(256) void k_dense_dedup(PullArgs a) {
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t stride = a.stride;
-    const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
-    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t wave = (uint64_t)blockIdx.x * kDedupWaves + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kDedupWaves;
     const uint32_t npass = (a.wact + 127u) / 128u;
     unsigned long long snap_local = 0ull;
     uint32_t t_srd = 0, t_swr = 0, t_fwr = 0;  // wave-uniform traffic accounting
@@ -343,7 +347,7 @@ __global__ __launch_bounds__(256) void k_dense_dedup(PullArgs a) {
             if (tv[q]) atomicAdd(&a.acct[2 + q], (unsigned long long)tv[q]);
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
+    for (uint32_t i = threadIdx.x; i < a.wact; i += blockDim.x) {
         const unsigned long long x = s_new[i];
         if (!x) continue;
         const unsigned long long have = __hip_atomic_load(&a.live[a.wbase + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

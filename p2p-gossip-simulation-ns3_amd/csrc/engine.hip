@@ -462,6 +462,7 @@ inline uint32_t hint_stamp(int64_t t) { return 1u + (uint32_t)(((t % 255) + 255)
 struct gossip_engine {
     gossip_config cfg{};
     int device = 0;
+    int num_cus = 256;  // compute units of the device (launch sizing)
     hipStream_t stream = nullptr;
     bool have_graph = false, have_sched = false;
     // ---- graph
@@ -658,6 +659,22 @@ struct gossip_engine {
     int64_t packed_tick = -1;        // host-staged export: message of (tick, chunk) already packed
     uint32_t packed_chunk = 0;
     void chunk_rows(uint32_t r, uint32_t c, uint64_t* lo, uint64_t* hi) const;
+    int pack_range(int64_t t, uint64_t lo, uint64_t hi, uint32_t wlive, hipStream_t s);
+    int unpack_range(int64_t t, uint64_t lo, uint64_t hi, uint32_t wlive, const uint64_t* msg, uint64_t words,
+                     hipStream_t s);
+    // Row-partition rehearsal (option rehearse_rows = R, one unpartitioned CSR engine): the pull
+    // runs as R row-range launches, and every range's F_next rows go through the real pack and
+    // unpack kernels (into the same rows: idempotent), each step timed per range -- one rank's
+    // compute and exchange work of an R-rank partition, on one GPU, with the data of the whole.
+    int64_t opt_rehearse_rows = 0;
+    std::vector<uint64_t> rr_lo;  // R + 1 range bounds (512-row blocks, set_row_partition's rule)
+    struct RehearseEv { uint32_t range, kind; hipEvent_t a, b; };  // kind 0 pull, 1 pack, 2 unpack
+    std::vector<RehearseEv> rr_events;
+    std::vector<double> rr_ms[3];
+    std::vector<uint64_t> rr_bytes;
+    uint64_t rr_ticks = 0;
+    int rehearse_exchange(int64_t t);
+    void rehearse_harvest();
     int ensure_xstream();
     int retire_from(int64_t known_tick, const unsigned long long* live);
     int alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t);
@@ -895,7 +912,8 @@ int gossip_engine::alloc_device() {
     stride = (words + kTileWords - 1) / kTileWords * kTileWords;  // rows start on 128-B lines
     // Young tiles: the CSR tick pull on graphs whose frontier rows outgrow the caches (C3/C4).
     {
-        const bool ok = !dense && !batch && !handshake && row_count == 1 && !(cfg.flags & GOSSIP_F_NOSKIP) &&
+        const bool ok = !dense && !batch && !handshake && row_count == 1 && opt_rehearse_rows <= 1 &&
+                        !(cfg.flags & GOSSIP_F_NOSKIP) &&
                         n < (1u << 31);  // (peer ids carry a hint in bit 31)
         if (opt_young == 1 && !ok)
             return set_error(GOSSIP_EINVAL, "young tiles need the CSR tick engine (not DENSE, HOP_BATCH, "
@@ -935,6 +953,13 @@ int gossip_engine::alloc_device() {
     const uint64_t bm = (uint64_t)n * stride * 8;
     // seen rows: a row-partitioned rank dedups only its own rows (F_cur / F_next stay whole: the
     // pull reads every peer's row, the exchange writes the other ranks' rows)
+    rr_lo.clear();
+    if (opt_rehearse_rows > 1) {  // rehearsal ranges: set_row_partition's blocks (ceil(n / R) -> 512 rows)
+        if (dense) return set_error(GOSSIP_EINVAL, "rehearse_rows: CSR engines only");
+        const uint64_t R = (uint64_t)opt_rehearse_rows;
+        const uint64_t rpr = ((uint64_t)(n + R - 1) / R + 511) / 512 * 512;
+        for (uint64_t r = 0; r <= R; r++) rr_lo.push_back(std::min<uint64_t>(n, r * rpr));
+    }
     seen_lo = row_count > 1 ? v0 : 0u;
     seen_n = row_count > 1 ? v1 - v0 : n;
     const uint64_t bm_seen = (uint64_t)seen_n * stride * 8;
@@ -1642,12 +1667,13 @@ int gossip_engine::tick_step_a(int64_t t) {
         // step, the grid sized to the rows (k_dense_dedup, dense_kernel.h)
         auto run_dedup = [&](const PullArgs& base) {
             const uint64_t rows = base.n > base.v0 ? base.n - base.v0 : 0;
-            const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((rows + 3) / 4, 4096));
+            const uint32_t g = (uint32_t)std::max<uint64_t>(
+                1, std::min<uint64_t>((rows + kDedupWaves - 1) / kDedupWaves, 2u * (uint32_t)num_cus));
             for (uint32_t wb = 0; wb < wact; wb += kPullLdsWords) {
                 PullArgs c = base;
                 c.wbase = wb;
                 c.wact = std::min(kPullLdsWords, wact - wb);
-                k_dense_dedup<<<g, 256, pull_lds_bytes(c.wact, c.keep_lds != 0), stream>>>(c);
+                k_dense_dedup<<<g, 64 * kDedupWaves, pull_lds_bytes(c.wact, c.keep_lds != 0), stream>>>(c);
             }
         };
         // the MFMA contraction of rows [lo, hi) (DENSE mode) into the incoming words
@@ -1711,6 +1737,29 @@ int gossip_engine::tick_step_a(int64_t t) {
             }
             a.inc = d_inc;
             run_dedup(a);
+        } else if (opt_rehearse_rows > 1 && !ny) {
+            // row-partition rehearsal: one pull launch per rank's row range, each timed
+            for (uint32_t r = 0; r + 1 < (uint32_t)rr_lo.size(); r++) {
+                PullArgs ar = a;
+                ar.v0 = (uint32_t)rr_lo[r];
+                ar.n = (uint32_t)rr_lo[r + 1];
+                if (ar.n <= ar.v0) continue;
+                hipEvent_t ra = nullptr, rb = nullptr;
+                if (cfg.flags & GOSSIP_F_TIMING) {
+                    ra = get_event();
+                    rb = get_event();
+                    HIP_TRY(hipEventRecord(ra, stream));
+                }
+                run_pull(ar, true);
+                if (cfg.flags & GOSSIP_F_TIMING) {
+                    HIP_TRY(hipEventRecord(rb, stream));
+                    rr_events.push_back({r, 0u, ra, rb});
+                }
+            }
+            if (cfg.flags & GOSSIP_F_TIMING) {
+                HIP_TRY(hipEventRecord(e1, stream));
+                timers.emplace_back(e0, e1);
+            }
         } else {
             if (overlap) {
                 HIP_TRY(hipEventRecord(ev_fork, stream));
@@ -1897,11 +1946,16 @@ int gossip_engine::ensure_dev(uint64_t*& p, uint64_t& cap, uint64_t words) {
 // Pack this rank's rows of chunk c of F_next (after the chunk's pull and births) into d_msg on
 // stream s; msg_words = size.  (One host wait: the row count sizes the message.)
 int gossip_engine::pack_rows(int64_t t, uint32_t c, hipStream_t s) {
-    const int nxt = fcur ^ 1, lv = (int)(t % 3);
     uint64_t lo, hi;
     chunk_rows(row_rank, c, &lo, &hi);
-    const uint64_t k = hi - lo;
     const uint32_t wlive = (c == kWholeRows || c + 1 >= nchunks) ? hw : 0u;  // liveness: last chunk
+    return pack_range(t, lo, hi, wlive, s);
+}
+
+// Pack rows [lo, hi) of F_next (+ `wlive` liveness words) into d_msg on stream s.
+int gossip_engine::pack_range(int64_t t, uint64_t lo, uint64_t hi, uint32_t wlive, hipStream_t s) {
+    const int nxt = fcur ^ 1, lv = (int)(t % 3);
+    const uint64_t k = hi - lo;
     int rc = ensure_dev(d_msg, msg_cap, pack_layout(k, ntw, 0, wlive).rows);
     if (rc) return rc;
     if (k + 1 > cnt_cap) {
@@ -1954,15 +2008,22 @@ int gossip_engine::pack_rows(int64_t t, uint32_t c, hipStream_t s) {
 // Unpack rank r's message of chunk c (device buffer, `words` long) into this engine's F_next,
 // nz_next and (last chunk) liveness, on stream s.  No host wait.
 int gossip_engine::unpack_rows(int64_t t, uint32_t r, uint32_t c, const uint64_t* msg, uint64_t words, hipStream_t s) {
-    const int nxt = fcur ^ 1, lv = (int)(t % 3);
     uint64_t lo, hi;
     chunk_rows(r, c, &lo, &hi);
-    const uint64_t k = hi - lo;
     const uint32_t wlive = (c == kWholeRows || c + 1 >= nchunks) ? hw : 0u;
-    const PackLayout L0 = pack_layout(k, ntw, 0, wlive);
+    const PackLayout L0 = pack_layout(hi - lo, ntw, 0, wlive);
     if (words < L0.total || (words - L0.total) % 16u)
         return set_error(GOSSIP_EINVAL, "row exchange: message of rank " + std::to_string(r) +
                                             " has the wrong size (ranks diverged?)");
+    return unpack_range(t, lo, hi, wlive, msg, words, s);
+}
+
+// Unpack a message of rows [lo, hi) (+ `wlive` liveness words) into F_next / nz_next / liveness.
+int gossip_engine::unpack_range(int64_t t, uint64_t lo, uint64_t hi, uint32_t wlive, const uint64_t* msg,
+                                uint64_t words, hipStream_t s) {
+    const int nxt = fcur ^ 1, lv = (int)(t % 3);
+    const uint64_t k = hi - lo;
+    const PackLayout L0 = pack_layout(k, ntw, 0, wlive);
     const uint64_t total = (words - L0.total) / 16u;
     const PackLayout L = pack_layout(k, ntw, total, wlive);
     if (k) HIP_TRY(hipMemcpyAsync(d_nz[nxt] + lo * ntw, msg + L.nz, (size_t)k * ntw * 8, hipMemcpyDeviceToDevice, s));
@@ -1979,6 +2040,51 @@ int gossip_engine::unpack_rows(int64_t t, uint32_t r, uint32_t c, const uint64_t
     }
     exchange_bytes_in += words * 8;
     return GOSSIP_OK;
+}
+
+// Rehearsal of the row exchange (option rehearse_rows): every range's F_next rows are packed
+// into its message and unpacked again into the same rows (the data are unchanged), so a range's
+// pack time, its message size and its unpack time -- what every OTHER rank spends on it -- are
+// measured with the real kernels.
+int gossip_engine::rehearse_exchange(int64_t t) {
+    const bool timing = (cfg.flags & GOSSIP_F_TIMING) != 0;
+    const uint32_t R = (uint32_t)rr_lo.size() - 1;
+    if (rr_bytes.size() != R) rr_bytes.assign(R, 0);
+    for (uint32_t r = 0; r < R; r++) {
+        const uint64_t lo = rr_lo[r], hi = rr_lo[r + 1];
+        if (hi <= lo) continue;
+        hipEvent_t a = timing ? get_event() : nullptr, b = timing ? get_event() : nullptr;
+        if (timing) HIP_TRY(hipEventRecord(a, stream));
+        int rc = pack_range(t, lo, hi, hw, stream);
+        if (rc) return rc;
+        if (timing) {
+            HIP_TRY(hipEventRecord(b, stream));
+            rr_events.push_back({r, 1u, a, b});
+        }
+        rr_bytes[r] += msg_words * 8;
+        hipEvent_t c = timing ? get_event() : nullptr, d = timing ? get_event() : nullptr;
+        if (timing) HIP_TRY(hipEventRecord(c, stream));
+        if ((rc = unpack_range(t, lo, hi, hw, d_msg, msg_words, stream))) return rc;
+        if (timing) {
+            HIP_TRY(hipEventRecord(d, stream));
+            rr_events.push_back({r, 2u, c, d});
+        }
+    }
+    rr_ticks++;
+    return GOSSIP_OK;
+}
+
+void gossip_engine::rehearse_harvest() {
+    const uint32_t R = rr_lo.empty() ? 0u : (uint32_t)rr_lo.size() - 1;
+    for (auto& v : rr_ms)
+        if (v.size() != R) v.assign(R, 0.0);
+    for (const RehearseEv& x : rr_events) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, x.a, x.b) == hipSuccess && x.range < R) rr_ms[x.kind][x.range] += ms;
+        event_pool.push_back(x.a);
+        event_pool.push_back(x.b);
+    }
+    rr_events.clear();
 }
 
 // Row partition over RCCL, pipelined: for every row chunk, once the engine stream has pulled it
@@ -2026,6 +2132,9 @@ int gossip_engine::tick_step_b(int64_t t) {
     const int nxt = fcur ^ 1;
     if (comm) {
         int rc = exchange_rccl(t);
+        if (rc) return rc;
+    } else if (opt_rehearse_rows > 1 && !young && hw) {
+        int rc = rehearse_exchange(t);
         if (rc) return rc;
     }
     if (xstream) {  // the unpacked rows and liveness precede the read-back and the next pull
@@ -2132,6 +2241,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->device = cfg->device;
         HIP_TRY(hipSetDevice(e->device));
         HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+        HIP_TRY(hipDeviceGetAttribute(&e->num_cus, hipDeviceAttributeMultiprocessorCount, e->device));
         e->L = cfg->latency_ns;
         e->t0 = cfg->t_start_ns;
         e->tick0 = cfg->t_start_ns / e->L;
@@ -2448,6 +2558,12 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
         if (value < 1 || value > (int64_t)gossip_engine::kMaxChunks) return set_error(GOSSIP_EINVAL, "xchunks: 1 .. 16 row chunks");
         if (e->tick_open) return set_error(GOSSIP_ESTATE, "xchunks: not between tick_begin and tick_end");
         e->opt_xchunks = value;
+    } else if (k == "rehearse_rows") {
+        if (value < 0 || value > 64) return set_error(GOSSIP_EINVAL, "rehearse_rows: 0 (off) .. 64 row ranges");
+        if (e->have_sched) return set_error(GOSSIP_ESTATE, "rehearse_rows: set before the schedule");
+        if (value > 1 && e->row_count > 1)
+            return set_error(GOSSIP_EINVAL, "rehearse_rows: an unpartitioned CSR engine");
+        e->opt_rehearse_rows = value;
     } else if (k == "dense_min_tiles") {
         if (value < 1) return set_error(GOSSIP_EINVAL, "dense_min_tiles >= 1");
         e->opt_dense_min_tiles = value;
@@ -2897,6 +3013,24 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     return GOSSIP_OK;
 }
 
+int gossip_engine_get_rehearsal(gossip_engine* e, uint32_t ranges, double* pull_ms, double* pack_ms,
+                                double* unpack_ms, uint64_t* msg_bytes, uint64_t* ticks) {
+    if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    if (e->opt_rehearse_rows < 2 || ranges != (uint32_t)e->opt_rehearse_rows)
+        return set_error(GOSSIP_EINVAL, "get_rehearsal: ranges must equal the rehearse_rows option");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->rehearse_harvest();
+    for (uint32_t r = 0; r < ranges; r++) {
+        if (pull_ms) pull_ms[r] = e->rr_ms[0][r];
+        if (pack_ms) pack_ms[r] = e->rr_ms[1][r];
+        if (unpack_ms) unpack_ms[r] = e->rr_ms[2][r];
+        if (msg_bytes) msg_bytes[r] = r < e->rr_bytes.size() ? e->rr_bytes[r] : 0;
+    }
+    if (ticks) *ticks = e->rr_ticks;
+    return GOSSIP_OK;
+}
+
 int gossip_engine_reset_timing(gossip_engine* e) {
     if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
     HIP_TRY(hipSetDevice(e->device));
@@ -2922,6 +3056,10 @@ int gossip_engine_reset_timing(gossip_engine* e) {
     }
     e->timers_phase.clear();
     e->phase_ms_done = 0.0;
+    e->rehearse_harvest();  // (row-partition rehearsal: restart the per-range sums)
+    for (auto& v : e->rr_ms) std::fill(v.begin(), v.end(), 0.0);
+    std::fill(e->rr_bytes.begin(), e->rr_bytes.end(), 0ull);
+    e->rr_ticks = 0;
     if (e->d_acct) {
         HIP_TRY(hipMemsetAsync(e->d_acct, 0, 16 * 8, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));

@@ -195,11 +195,15 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                 // (a dead pair's seen words are never needed: only cleared, never merged)
                 const uint64_t v1 = c0 + step1 * NPW + slot;
                 const uint32_t lw1 = pass1 * 2u * LPW + 2u * wl;
+                // this item's peer range, read with the whole wave active: a shuffle inside the
+                // branch below would read the row pointers of lanes whose own pair is dead
+                // (inactive lanes give no data), so a node with more peers than one lane group
+                // could pass the one-group test below and be gated on a partial occupancy OR
+                const uint32_t ix = step * NPW + slot;
+                const int32_t b0 = __shfl((int)rp, (int)ix, 64);
+                const int32_t e0 = ix + 1u < 64u ? __shfl((int)rp, (int)((ix + 1u) & 63u), 64) : (int32_t)rp_end;
                 if (v1 < n && lw1 < a.wact && (s_lp[lw1] | s_lp[lw1 + 1u]) != 0ull) {
                     // same node and occupancy word as this item, peers in one lane group
-                    const uint32_t ix = step * NPW + slot;
-                    const int32_t b0 = __shfl((int)rp, (int)ix, 64);
-                    const int32_t e0 = ix + 1u < 64u ? __shfl((int)rp, (int)((ix + 1u) & 63u), 64) : (int32_t)rp_end;
                     s2n_gated = gate && step1 == step &&
                                 ((a.wbase + lw1) >> 10) == ((a.wbase + pass * 2u * LPW) >> 10) && e0 - b0 <= GRP &&
                                 !((nzor >> (((a.wbase + lw1) >> 4) & 63u)) & 1ull);

@@ -60,7 +60,7 @@ EXPORTED_SYMBOLS = (
     "gossip_schedule_create_philox", "gossip_engine_exchange_chunks",
     "gossip_engine_exchange_export_chunk", "gossip_engine_exchange_import_chunk",
     "gossip_format_netanim", "gossip_topology_load_links", "gossip_schedule_load_events",
-    "gossip_engine_abort",
+    "gossip_engine_abort", "gossip_engine_get_rehearsal",
 )
 
 # NS-3 5 Mbps point-to-point links (p2pnetwork.cc:113): ns per byte, PPP+IPv4+TCP(timestamp
@@ -138,6 +138,7 @@ def load_library(path: str = LIB_PATH):
         "gossip_topology_load_links": (C.c_int, [u32, C.c_char_p, C.POINTER(P)]),
         "gossip_schedule_load_events": (C.c_int, [u32, C.c_char_p, C.POINTER(P)]),
         "gossip_engine_abort": (C.c_int, [P]),
+        "gossip_engine_get_rehearsal": (C.c_int, [P, u32, P, P, P, P, C.POINTER(u64)]),
         "gossip_topology_num_nodes": (u32, [P]),
         "gossip_topology_num_links": (u64, [P]),
         "gossip_topology_get_links": (C.c_int, [P, P, P]),
@@ -528,6 +529,16 @@ class Engine:
 
     def reset_timing(self):
         _check(load_library().gossip_engine_reset_timing(self._h), "reset timing")
+
+    def rehearsal(self, ranges: int) -> dict:
+        """Option rehearse_rows = ranges: per row block, summed since reset_timing -- pull, pack
+        and unpack time (ms) and message bytes, and the number of ticks rehearsed."""
+        pull, pack, unpack = (np.zeros(ranges) for _ in range(3))
+        msg = np.zeros(ranges, np.uint64)
+        ticks = C.c_uint64()
+        _check(load_library().gossip_engine_get_rehearsal(self._h, ranges, _vp(pull), _vp(pack), _vp(unpack),
+                                                          _vp(msg), C.byref(ticks)), "rehearsal")
+        return dict(pull_ms=pull, pack_ms=pack, unpack_ms=unpack, msg_bytes=msg, ticks=int(ticks.value))
 
     def trace(self):
         lib = load_library()

@@ -80,3 +80,25 @@ def test_late_exit_reads_fewer_rows(gossip):
     for k in STATS:
         assert np.array_equal(getattr(runs[0][0], k), getattr(runs[4][0], k)), k
     assert runs[4][1].pull_pair_edges < runs[0][1].pull_pair_edges
+
+
+@pytest.mark.parametrize("gate", [1, 0])
+def test_seen_gate_with_wide_peer_lists(gossip, oracle, gate):
+    # k_pull<32, 1> (windows wider than 64 words) serves a node with one 32-lane group; nodes
+    # with more peers than that must never be gated on the first group's occupancy alone (the
+    # occupancy gate of the own-seen loads, option pull_gate; a C3 run lost receptions at
+    # 37-peer nodes when the one-group test read the row pointers of inactive lanes).  Average
+    # degree 40: most nodes have > 32 peers.
+    n = 3000
+    topo = gossip.Topology.gnp(n, 40.0 / (n - 1), 95, gossip.TOPO_EXACT)
+    lat = gossip.milliseconds_to_ns(5.0)
+    t_cut = gossip.seconds_to_ns(5.6)
+    ev = gossip.make_schedule(n, 96, T0, t_cut)
+    eng = _engine(gossip, topo, ev, lat, t_cut, dict(pull_gate=gate, young=0), gossip.F_TILE_PER_TICK)
+    st = eng.stats()
+    assert eng.counters().words_hw > 64  # the one-group-per-node pull
+    eng.close()
+    a, b = topo.links()
+    r = oracle.run_replay(n, lat, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
+    for k in STATS:
+        assert np.array_equal(getattr(st, k), getattr(r, k)), (gate, k)

@@ -163,3 +163,28 @@ def test_hybrid_share_shards_by_row_ranks(gossip, mode, p):
     for k in SUM:
         total = sum(getattr(g, k).astype(np.uint64) for g in parts)
         assert np.array_equal(total, getattr(want, k).astype(np.uint64)), k
+
+
+def test_rehearse_rows_keeps_results(gossip):
+    # option rehearse_rows (one GPU stands in for one rank of an R-rank partition: per-block pull
+    # launches, every block's rows packed and unpacked again) must not change a single counter
+    n = 5000
+    topo, t_cut, ev = _inputs(gossip, n, 0.004, 81, 6.6)
+    want = _engine(gossip, n, t_cut, topo, ev, gossip.MODE_CSR, 0)
+    want.run()
+    w = want.stats()
+    want.close()
+    e = gossip.Engine(n, L, T0, t_cut, flags=gossip.F_TIMING)
+    e.set_option("rehearse_rows", 3)
+    e.set_topology(topo)
+    e.set_schedule(ev)
+    e.reset_timing()
+    e.run()
+    e.sync()
+    got = e.stats()
+    rh = e.rehearsal(3)
+    e.close()
+    for k in SUM + ("peers", "sockets"):
+        assert np.array_equal(getattr(got, k), getattr(w, k)), k
+    assert rh["ticks"] > 100 and (rh["pull_ms"] > 0).all() and (rh["msg_bytes"] > 0).all()
+    assert (rh["pack_ms"] > 0).all() and (rh["unpack_ms"] > 0).all()
