@@ -107,7 +107,7 @@ __global__ __launch_bounds__(512, 1) void k_dense_bits(BitsArgs a) {
         const unsigned long long lv = a.live_prev[w0] | a.live_prev[w0 + 1] | a.live_prev[w0 + 2] |
                                       a.live_prev[w0 + 3];
         if (lv == 0ull) {
-            if (t == 0 && a.acct) atomicAdd(&a.acct[6], 1ull);
+            if (t == 0 && a.acct) acct_add(a.acct, 6, 1ull);
             return;
         }
     }
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(512, 1) void k_dense_bits(BitsArgs a) {
         }
     }
     if (t == 0 && a.acct && computed)
-        atomicAdd(&a.acct[5], 2ull * kDenseTile * kDenseTile * kStageK * computed);
+        acct_add(a.acct, 5, 2ull * kDenseTile * kDenseTile * kStageK * computed);
     if (computed == 0) return;
     // ---- epilogue: Inc > 0 -> one 64-bit word per row (wave ballots), OR into inc ----
     // lane l collects rows l (lo) and l + 64 (hi) of the wave's 128
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(1024) void k_dense_dedup(PullArgs a) {
         const uint32_t tv[3] = {t_srd, t_swr, t_fwr};
 #pragma unroll
         for (int q = 0; q < 3; q++)
-            if (tv[q]) atomicAdd(&a.acct[2 + q], (unsigned long long)tv[q]);
+            if (tv[q]) acct_add(a.acct, 2 + q, (unsigned long long)tv[q]);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < a.wact; i += blockDim.x) {

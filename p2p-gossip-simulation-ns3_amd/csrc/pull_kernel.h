@@ -468,7 +468,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
         const int slot_of[6] = {0, 1, 2, 3, 4, 7};
 #pragma unroll
         for (int q = 0; q < 6; q++)
-            if (tv[q]) atomicAdd(&a.acct[slot_of[q]], (unsigned long long)tv[q]);
+            if (tv[q]) acct_add(a.acct, (uint32_t)slot_of[q], (unsigned long long)tv[q]);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
@@ -718,7 +718,7 @@ __global__ __launch_bounds__(256) void k_pull_wide(PullArgs a) {
         const int slot_of[6] = {0, 1, 2, 3, 4, 7};
 #pragma unroll
         for (int q = 0; q < 6; q++)
-            if (tv[q]) atomicAdd(&a.acct[slot_of[q]], (unsigned long long)tv[q]);
+            if (tv[q]) acct_add(a.acct, (uint32_t)slot_of[q], (unsigned long long)tv[q]);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {

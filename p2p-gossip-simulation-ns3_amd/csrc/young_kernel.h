@@ -423,6 +423,6 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
         const uint32_t tv[8] = {t_sl, t_col, t_fb, t_srd, t_swr, t_rw, t_slw, t_miss};
 #pragma unroll
         for (int q = 0; q < 8; q++)
-            if (tv[q]) atomicAdd(&a.acct[8 + q], (unsigned long long)tv[q]);
+            if (tv[q]) acct_add(a.acct, 8 + q, (unsigned long long)tv[q]);
     }
 }
