@@ -34,7 +34,7 @@ def late_case(gossip, oracle):
     n = 6000
     topo = gossip.Topology.gnp(n, 16.0 / (n - 1), 91, gossip.TOPO_SKIP)
     lat = gossip.milliseconds_to_ns(5.0)
-    t_cut = gossip.seconds_to_ns(7.37)  # a cut inside a tick: keep masks on late words
+    t_cut = gossip.seconds_to_ns(6.37)  # a cut inside a tick: keep masks on late words
     ev = gossip.make_schedule(n, 92, T0, t_cut, id_mask=0x3FFF)  # id groups
     a, b = topo.links()
     r = oracle.run_replay(n, lat, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=True)
