@@ -650,6 +650,20 @@ struct gossip_engine {
     uint64_t* d_recv_msgs = nullptr;  // the other ranks' messages (RCCL / host-staged import)
     uint64_t recv_cap = 0;
     uint64_t* d_sizes = nullptr;
+    // RCCL exchange with device-side sizes (exchange_rccl): per (rank, chunk) a row capacity that
+    // every rank derives from the same all-gathered row counts, so each broadcast's length is known
+    // without reading the message first; rows beyond it go in a second round after the tick's one
+    // host wait.
+    std::vector<uint64_t> xcap;          // [r * kMaxChunks + c] rows
+    uint64_t* d_tot = nullptr;           // all-gathered row counts of the tick [c * row_count + r]
+    uint64_t* h_tot = nullptr;           // pinned copy
+    uint64_t* d_ovf = nullptr;           // overflow rows received in the second round
+    uint64_t ovf_cap = 0;
+    bool xchunks_checked = false;
+    uint64_t x_overflow_rounds = 0;      // (rank, chunk) messages that needed a second round
+    int pack_dev(int64_t t, uint64_t lo, uint64_t hi, uint32_t wlive, hipStream_t s);
+    int unpack_dev(int64_t t, uint64_t lo, uint64_t hi, uint32_t wlive, const uint64_t* msg, const uint64_t* rows,
+                   uint64_t r0, uint64_t r1, bool prefix, hipStream_t s);
     uint64_t sizes_cap = 0;
     std::atomic<bool> aborted{false};  // gossip_engine_abort: comm torn down by another thread
     uint64_t exchange_bytes_out = 0, exchange_bytes_in = 0;
@@ -709,6 +723,7 @@ gossip_engine::~gossip_engine() {
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     hipFree(d_msg); hipFree(d_cnt); hipFree(d_scan_tmp); hipFree(d_recv_msgs); hipFree(d_sizes);
+    hipFree(d_tot); hipFree(d_ovf); hipHostFree(h_tot);
     hipFree(d_slot[0]); hipFree(d_slot[1]);
     hipFree(d_rev); hipFree(d_hint[0]); hipFree(d_hint[1]);
     for (int k = 0; k < kRing; k++) { hipFree(d_young[k]); hipHostFree(h_young[k]); }
@@ -1898,16 +1913,22 @@ __global__ __launch_bounds__(256) void k_pack_count(const unsigned long long* __
     cnt[i] = c;
 }
 
-// one wave per node: its occupied tile rows, 4 rows per instruction (16 lanes x 8 B each)
+// one wave per node: its occupied tile rows, 4 rows per instruction (16 lanes x 8 B each).
+// Only message rows [r0, r1) move (r1 capped by *total when total is given: the row count read on
+// the device from a message header); `rows` points at message row r0.
 template <bool PACK>
 __global__ __launch_bounds__(256) void k_move_rows(uint64_t* __restrict__ F, uint32_t stride, uint64_t lo, uint64_t k,
                                                    const uint64_t* __restrict__ nz, uint32_t ntw,
-                                                   const uint32_t* __restrict__ off, uint64_t* __restrict__ rows) {
+                                                   const uint32_t* __restrict__ off, uint64_t* __restrict__ rows,
+                                                   uint64_t r0 = 0, uint64_t r1 = ~0ull,
+                                                   const uint64_t* __restrict__ total = nullptr) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    if (total) r1 = min(r1, *total);
     for (uint64_t i = wave; i < k; i += nwaves) {
         uint64_t o = off[i];
+        if (o >= r1) break;  // (offsets grow with i)
         for (uint32_t w = 0; w < ntw; w++) {
             unsigned long long m = (unsigned long long)nz[i * ntw + w];
             while (m) {
@@ -1916,10 +1937,10 @@ __global__ __launch_bounds__(256) void k_move_rows(uint64_t* __restrict__ F, uin
                 unsigned long long mm = m;
                 for (uint32_t r = 0; r < g && mm; r++) mm &= mm - 1ull;
                 const uint32_t cntb = (uint32_t)min(4, __popcll(m));
-                if (g < cntb) {
+                if (g < cntb && o + g >= r0 && o + g < r1) {
                     const uint32_t tile = w * 64u + (uint32_t)__builtin_ctzll(mm);
                     uint64_t* frow = F + (lo + i) * stride + (uint64_t)tile * 16u + (lane & 15u);
-                    uint64_t* mrow = rows + (o + g) * 16u + (lane & 15u);
+                    uint64_t* mrow = rows + (o + g - r0) * 16u + (lane & 15u);
                     if (PACK) *mrow = *frow;
                     else *frow = *mrow;
                 }
@@ -1933,6 +1954,24 @@ __global__ __launch_bounds__(256) void k_move_rows(uint64_t* __restrict__ F, uin
 __global__ void k_or_words(const uint64_t* __restrict__ src, uint32_t n, unsigned long long* __restrict__ dst) {
     const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w < n && src[w]) dst[w] |= src[w];
+}
+
+// message header = its row count, the exclusive scan's last element (the RCCL exchange reads it
+// on the device: no host wait per chunk)
+__global__ void k_msg_header(const uint32_t* __restrict__ off_end, uint64_t* __restrict__ hdr) { *hdr = *off_end; }
+
+// RCCL message layout: a fixed prefix (header, occupancy words, row offsets, liveness) whose size
+// every rank knows, then the rows; a broadcast carries the prefix and up to `cap` rows
+struct DevLayout {
+    uint64_t nz, off, live, rows;  // rows = prefix words
+};
+DevLayout dev_layout(uint64_t k, uint32_t ntw, uint32_t wlive) {
+    DevLayout L;
+    L.nz = 1;
+    L.off = L.nz + k * ntw;
+    L.live = L.off + (k + 2) / 2;
+    L.rows = L.live + wlive;
+    return L;
 }
 
 #define NCCL_TRY(x)                                                                         \
@@ -2096,41 +2135,176 @@ void gossip_engine::rehearse_harvest() {
     rr_events.clear();
 }
 
-// Row partition over RCCL, pipelined: for every row chunk, once the engine stream has pulled it
-// (ev_chunk[c]), the exchange stream packs it, all-gathers the message sizes (and chunk counts),
-// broadcasts every rank's message (an all-gather with per-rank sizes) and unpacks the others'
-// chunk c -- while the engine stream already pulls chunk c + 1.  The engine stream joins the
-// exchange stream before the tick's liveness read-back (tick_step_b).
+// Pack rows [lo, hi) of F_next into d_msg in the device-sized layout (dev_layout; the header = the
+// row count, written on the device): no host wait.  d_msg holds the worst case, every tile row.
+int gossip_engine::pack_dev(int64_t t, uint64_t lo, uint64_t hi, uint32_t wlive, hipStream_t s) {
+    const int nxt = fcur ^ 1, lv = (int)(t % 3);
+    const uint64_t k = hi - lo;
+    const DevLayout L = dev_layout(k, ntw, wlive);
+    int rc = ensure_dev(d_msg, msg_cap, L.rows + 16ull * k * (hw / kTileWords));
+    if (rc) return rc;
+    if (k + 1 > cnt_cap) {
+        HIP_TRY(hipStreamSynchronize(s));
+        hipFree(d_cnt);
+        cnt_cap = k + 1;
+        HIP_TRY(hipMalloc(&d_cnt, cnt_cap * 4));
+    }
+    uint32_t* off = reinterpret_cast<uint32_t*>(d_msg + L.off);
+    k_pack_count<<<(uint32_t)((k + 1 + 255) / 256), 256, 0, s>>>(d_nz[nxt] + lo * ntw, k, ntw, d_msg + L.nz, d_cnt);
+    HIP_TRY(hipGetLastError());
+    size_t tmp = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d_cnt, off, (int)(k + 1), s));
+    if (tmp > scan_tmp_bytes) {  // (first use of a chunk size only)
+        HIP_TRY(hipStreamSynchronize(s));
+        hipFree(d_scan_tmp);
+        scan_tmp_bytes = tmp;
+        HIP_TRY(hipMalloc(&d_scan_tmp, tmp));
+    }
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(d_scan_tmp, tmp, d_cnt, off, (int)(k + 1), s));
+    k_msg_header<<<1, 1, 0, s>>>(off + k, d_msg);
+    const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((k + 3) / 4, 4096));
+    k_move_rows<true><<<g, 256, 0, s>>>(d_F[nxt], stride, lo, k, d_msg + L.nz, ntw, off, d_msg + L.rows);
+    HIP_TRY(hipGetLastError());
+    if (wlive) HIP_TRY(hipMemcpyAsync(d_msg + L.live, d_live[lv], (size_t)wlive * 8, hipMemcpyDeviceToDevice, s));
+    return GOSSIP_OK;
+}
+
+// Unpack message rows [r0, r1) of another rank's rows [lo, hi): `msg` is its prefix (header,
+// occupancy, offsets, liveness), `rows` points at message row r0.  prefix: first round -- also
+// the occupancy and liveness words, and r1 capped by the header's row count on the device.
+int gossip_engine::unpack_dev(int64_t t, uint64_t lo, uint64_t hi, uint32_t wlive, const uint64_t* msg,
+                              const uint64_t* rows, uint64_t r0, uint64_t r1, bool prefix, hipStream_t s) {
+    const int nxt = fcur ^ 1, lv = (int)(t % 3);
+    const uint64_t k = hi - lo;
+    const DevLayout L = dev_layout(k, ntw, wlive);
+    if (prefix && k)
+        HIP_TRY(hipMemcpyAsync(d_nz[nxt] + lo * ntw, msg + L.nz, (size_t)k * ntw * 8, hipMemcpyDeviceToDevice, s));
+    if (r1 > r0 && k) {
+        const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((k + 3) / 4, 4096));
+        k_move_rows<false><<<g, 256, 0, s>>>(d_F[nxt], stride, lo, k, msg + L.nz, ntw,
+                                             reinterpret_cast<const uint32_t*>(msg + L.off),
+                                             const_cast<uint64_t*>(rows), r0, r1, prefix ? msg : nullptr);
+        HIP_TRY(hipGetLastError());
+    }
+    if (prefix && wlive) {
+        k_or_words<<<(wlive + 255) / 256, 256, 0, s>>>(msg + L.live, wlive, d_live[lv]);
+        HIP_TRY(hipGetLastError());
+    }
+    return GOSSIP_OK;
+}
+
+// Row partition over RCCL, pipelined, with device-side sizes.  Per row chunk c, once the engine
+// stream has pulled it (ev_chunk[c]), the exchange stream packs the rank's rows (row count in the
+// message header, on the device), all-gathers the ranks' row counts into d_tot (device), and
+// broadcasts every rank's message prefix + its first xcap[r][c] rows -- a length every rank
+// derives from earlier ticks' counts, so no host wait -- then unpacks the others' chunk c (rows
+// capped by their header) while the engine stream pulls chunk c + 1.  After the last chunk: ONE
+// host wait reads the tick's counts; rows beyond a capacity (the first ticks, a growing frontier)
+// go in a second round (re-pack, broadcast the tail, unpack), and the capacities grow to 1.25x.
+// The engine stream joins the exchange stream before the tick's liveness read-back (tick_step_b).
 int gossip_engine::exchange_rccl(int64_t t) {
     int rc = ensure_xstream();
     if (rc) return rc;
-    if ((rc = ensure_dev(d_sizes, sizes_cap, 2 * row_count))) return rc;
-    std::vector<unsigned long long> sz(2 * row_count);
-    for (uint32_t c = 0; c < nchunks; c++) {
-        HIP_TRY(hipStreamWaitEvent(xstream, ev_chunk[c], 0));
-        if ((rc = pack_rows(t, c, xstream))) return rc;
-        const unsigned long long mine[2] = {msg_words, nchunks};
-        HIP_TRY(hipMemcpyAsync(d_sizes + 2 * row_rank, mine, 16, hipMemcpyHostToDevice, xstream));
-        NCCL_TRY(ncclAllGather(d_sizes + 2 * row_rank, d_sizes, 2, ncclUint64, comm, xstream));
-        HIP_TRY(hipMemcpyAsync(sz.data(), d_sizes, 2 * row_count * 8, hipMemcpyDeviceToHost, xstream));
+    const uint32_t R = row_count;
+    if (xcap.size() != (size_t)R * kMaxChunks) xcap.assign((size_t)R * kMaxChunks, 0ull);
+    if (!d_tot) {
+        HIP_TRY(hipMalloc(&d_tot, (size_t)R * kMaxChunks * 8));
+        HIP_TRY(hipHostMalloc(&h_tot, (size_t)R * kMaxChunks * 8, hipHostMallocDefault));
+    }
+    if (!xchunks_checked) {  // once: every rank must issue the same collectives per tick
+        if ((rc = ensure_dev(d_sizes, sizes_cap, 2 * R))) return rc;
+        const unsigned long long mine = nchunks;
+        HIP_TRY(hipMemcpyAsync(d_sizes + row_rank, &mine, 8, hipMemcpyHostToDevice, xstream));
+        NCCL_TRY(ncclAllGather(d_sizes + row_rank, d_sizes, 1, ncclUint64, comm, xstream));
+        std::vector<unsigned long long> all(R);
+        HIP_TRY(hipMemcpyAsync(all.data(), d_sizes, R * 8, hipMemcpyDeviceToHost, xstream));
         HIP_TRY(hipStreamSynchronize(xstream));
-        uint64_t tot = 0;
-        std::vector<uint64_t> at(row_count);
-        for (uint32_t r = 0; r < row_count; r++) {
-            if (sz[2 * r + 1] != nchunks)
-                return set_error(GOSSIP_EINVAL, "row exchange: ranks use different xchunks options");
-            at[r] = tot;
-            tot += r == row_rank ? 0 : sz[2 * r];
+        for (uint32_t r = 0; r < R; r++)
+            if (all[r] != nchunks) return set_error(GOSSIP_EINVAL, "row exchange: ranks use different xchunks options");
+        xchunks_checked = true;
+    }
+    auto geom = [&](uint32_t r, uint32_t c, uint64_t* lo, uint64_t* hi, uint32_t* wl) {
+        chunk_rows(r, c, lo, hi);
+        *wl = (c + 1 >= nchunks) ? hw : 0u;  // liveness rides in the last chunk
+    };
+    // receive buffers for the whole tick: [c][r] prefix + capacity rows
+    std::vector<uint64_t> at((size_t)nchunks * R, 0ull);
+    uint64_t tot_words = 0;
+    for (uint32_t c = 0; c < nchunks; c++)
+        for (uint32_t r = 0; r < R; r++) {
+            if (r == row_rank) continue;
+            uint64_t lo, hi;
+            uint32_t wl;
+            geom(r, c, &lo, &hi, &wl);
+            at[(size_t)c * R + r] = tot_words;
+            tot_words += dev_layout(hi - lo, ntw, wl).rows + 16ull * xcap[(size_t)r * kMaxChunks + c];
         }
-        if ((rc = ensure_dev(d_recv_msgs, recv_cap, std::max<uint64_t>(tot, 1)))) return rc;
+    if ((rc = ensure_dev(d_recv_msgs, recv_cap, std::max<uint64_t>(tot_words, 1)))) return rc;
+    for (uint32_t c = 0; c < nchunks; c++) {
+        uint64_t lo, hi;
+        uint32_t wl;
+        geom(row_rank, c, &lo, &hi, &wl);
+        HIP_TRY(hipStreamWaitEvent(xstream, ev_chunk[c], 0));
+        if ((rc = pack_dev(t, lo, hi, wl, xstream))) return rc;
+        NCCL_TRY(ncclAllGather(d_msg, d_tot + (size_t)c * R, 1, ncclUint64, comm, xstream));
         NCCL_TRY(ncclGroupStart());
-        for (uint32_t r = 0; r < row_count; r++) {
-            uint64_t* buf = r == row_rank ? d_msg : d_recv_msgs + at[r];
-            NCCL_TRY(ncclBroadcast(buf, buf, sz[2 * r], ncclUint64, (int)r, comm, xstream));
+        for (uint32_t r = 0; r < R; r++) {
+            uint64_t rlo, rhi;
+            uint32_t rwl;
+            geom(r, c, &rlo, &rhi, &rwl);
+            const uint64_t words = dev_layout(rhi - rlo, ntw, rwl).rows + 16ull * xcap[(size_t)r * kMaxChunks + c];
+            uint64_t* buf = r == row_rank ? d_msg : d_recv_msgs + at[(size_t)c * R + r];
+            NCCL_TRY(ncclBroadcast(buf, buf, words, ncclUint64, (int)r, comm, xstream));
+            if (r == row_rank) exchange_bytes_out += words * 8;
+            else exchange_bytes_in += words * 8;
         }
         NCCL_TRY(ncclGroupEnd());
-        for (uint32_t r = 0; r < row_count; r++)
-            if (r != row_rank && (rc = unpack_rows(t, r, c, d_recv_msgs + at[r], sz[2 * r], xstream))) return rc;
+        for (uint32_t r = 0; r < R; r++) {
+            if (r == row_rank) continue;
+            uint64_t rlo, rhi;
+            uint32_t rwl;
+            geom(r, c, &rlo, &rhi, &rwl);
+            const uint64_t* msg = d_recv_msgs + at[(size_t)c * R + r];
+            if ((rc = unpack_dev(t, rlo, rhi, rwl, msg, msg + dev_layout(rhi - rlo, ntw, rwl).rows, 0,
+                                 xcap[(size_t)r * kMaxChunks + c], true, xstream)))
+                return rc;
+        }
+    }
+    // the tick's one host wait: every rank's row counts
+    HIP_TRY(hipMemcpyAsync(h_tot, d_tot, (size_t)nchunks * R * 8, hipMemcpyDeviceToHost, xstream));
+    HIP_TRY(hipStreamSynchronize(xstream));
+    for (uint32_t c = 0; c < nchunks; c++) {
+        for (uint32_t r = 0; r < R; r++) {
+            uint64_t& cap = xcap[(size_t)r * kMaxChunks + c];
+            const uint64_t tot = h_tot[(size_t)c * R + r];
+            if (tot <= cap) continue;
+            // second round (identical decision on every rank): rows [cap, tot) of rank r, chunk c
+            uint64_t rlo, rhi;
+            uint32_t rwl;
+            geom(r, c, &rlo, &rhi, &rwl);
+            const DevLayout L = dev_layout(rhi - rlo, ntw, rwl);
+            const uint64_t words = 16ull * (tot - cap);
+            if (r == row_rank) {
+                if ((rc = pack_dev(t, rlo, rhi, rwl, xstream))) return rc;  // (d_msg held a later chunk)
+                NCCL_TRY(ncclBroadcast(d_msg + L.rows + 16ull * cap, d_msg + L.rows + 16ull * cap, words, ncclUint64,
+                                       (int)r, comm, xstream));
+                exchange_bytes_out += words * 8;
+            } else {
+                if ((rc = ensure_dev(d_ovf, ovf_cap, words))) return rc;
+                NCCL_TRY(ncclBroadcast(d_ovf, d_ovf, words, ncclUint64, (int)r, comm, xstream));
+                exchange_bytes_in += words * 8;
+                if ((rc = unpack_dev(t, rlo, rhi, rwl, d_recv_msgs + at[(size_t)c * R + r], d_ovf, cap, tot, false,
+                                     xstream)))
+                    return rc;
+                HIP_TRY(hipStreamSynchronize(xstream));  // (d_ovf is reused by the next overflow)
+            }
+            x_overflow_rounds++;
+        }
+        for (uint32_t r = 0; r < R; r++) {  // capacities: 1.25x the largest count seen (rows)
+            uint64_t& cap = xcap[(size_t)r * kMaxChunks + c];
+            const uint64_t tot = h_tot[(size_t)c * R + r];
+            if (tot > cap) cap = tot + tot / 4 + 16;
+        }
     }
     return GOSSIP_OK;
 }
@@ -2487,25 +2661,63 @@ int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end
             for (uint32_t r = 1; r < count; r++)
                 if (es[r]->hw != e0->hw || es[r]->stride != e0->stride || es[r]->fcur != e0->fcur)
                     return set_error(GOSSIP_EINVAL, "row partition engines diverged (different inputs?)");
-            // the compressed exchange of the RCCL backend, chunk by chunk, with device-to-device
-            // reads (the ranks already ran one after another, so nothing overlaps here)
+            // the RCCL backend's exchange, chunk by chunk, with device-to-device copies in place of
+            // the collectives (the ranks already ran one after another, so nothing overlaps here):
+            // the same device-sized messages, capacities and second rounds as exchange_rccl
             for (uint32_t r = 1; r < count; r++)
                 if (es[r]->nchunks != e0->nchunks) return set_error(GOSSIP_EINVAL, "ranks use different xchunks options");
             for (uint32_t c = 0; c < e0->nchunks; c++) {
+                auto geom = [&](uint32_t r, uint64_t* lo, uint64_t* hi, uint32_t* wl) {
+                    e0->chunk_rows(r, c, lo, hi);
+                    *wl = (c + 1 >= e0->nchunks) ? e0->hw : 0u;
+                };
                 for (uint32_t r = 0; r < count; r++) {
-                    HIP_TRY(hipSetDevice(es[r]->device));
-                    int rc = es[r]->pack_rows(t, c, es[r]->stream);
+                    gossip_engine* e = es[r];
+                    if (e->xcap.size() != (size_t)count * gossip_engine::kMaxChunks)
+                        e->xcap.assign((size_t)count * gossip_engine::kMaxChunks, 0ull);
+                    uint64_t lo, hi;
+                    uint32_t wl;
+                    geom(r, &lo, &hi, &wl);
+                    int rc = e->pack_dev(t, lo, hi, wl, e->stream);
                     if (rc) return rc;
-                    HIP_TRY(hipStreamSynchronize(es[r]->stream));
+                    HIP_TRY(hipStreamSynchronize(e->stream));
                 }
+                std::vector<unsigned long long> tot(count);
+                for (uint32_t r = 0; r < count; r++)  // (the all-gather of the row counts)
+                    HIP_TRY(hipMemcpy(&tot[r], es[r]->d_msg, 8, hipMemcpyDeviceToHost));
                 for (uint32_t d = 0; d < count; d++) {
-                    HIP_TRY(hipSetDevice(es[d]->device));
+                    gossip_engine* e = es[d];
                     for (uint32_t r = 0; r < count; r++) {
                         if (r == d) continue;
-                        int rc = es[d]->unpack_rows(t, r, c, es[r]->d_msg, es[r]->msg_words, es[d]->stream);
+                        uint64_t lo, hi;
+                        uint32_t wl;
+                        geom(r, &lo, &hi, &wl);
+                        const DevLayout L = dev_layout(hi - lo, e->ntw, wl);
+                        const uint64_t cap = e->xcap[(size_t)r * gossip_engine::kMaxChunks + c];
+                        int rc = e->ensure_dev(e->d_recv_msgs, e->recv_cap, L.rows + 16ull * cap);
                         if (rc) return rc;
+                        // first round: prefix + the first `cap` rows (the header caps the unpack)
+                        HIP_TRY(hipMemcpyAsync(e->d_recv_msgs, es[r]->d_msg, (L.rows + 16ull * cap) * 8,
+                                               hipMemcpyDeviceToDevice, e->stream));
+                        if ((rc = e->unpack_dev(t, lo, hi, wl, e->d_recv_msgs, e->d_recv_msgs + L.rows, 0, cap, true,
+                                                e->stream)))
+                            return rc;
+                        if (tot[r] > cap) {  // second round: rows [cap, tot)
+                            const uint64_t words = 16ull * (tot[r] - cap);
+                            if ((rc = e->ensure_dev(e->d_ovf, e->ovf_cap, words))) return rc;
+                            HIP_TRY(hipMemcpyAsync(e->d_ovf, es[r]->d_msg + L.rows + 16ull * cap, words * 8,
+                                                   hipMemcpyDeviceToDevice, e->stream));
+                            if ((rc = e->unpack_dev(t, lo, hi, wl, e->d_recv_msgs, e->d_ovf, cap, tot[r], false,
+                                                    e->stream)))
+                                return rc;
+                            e->x_overflow_rounds++;
+                        }
+                        HIP_TRY(hipStreamSynchronize(e->stream));  // (receive buffers are reused)
                     }
-                    HIP_TRY(hipStreamSynchronize(es[d]->stream));
+                    for (uint32_t r = 0; r < count; r++) {
+                        uint64_t& cap = e->xcap[(size_t)r * gossip_engine::kMaxChunks + c];
+                        if (tot[r] > cap) cap = tot[r] + tot[r] / 4 + 16;
+                    }
                 }
             }
             for (uint32_t r = 0; r < count; r++) {
@@ -2566,6 +2778,7 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     } else if (k == "xchunks") {
         if (value < 1 || value > (int64_t)gossip_engine::kMaxChunks) return set_error(GOSSIP_EINVAL, "xchunks: 1 .. 16 row chunks");
         if (e->tick_open) return set_error(GOSSIP_ESTATE, "xchunks: not between tick_begin and tick_end");
+        if (e->comm) return set_error(GOSSIP_ESTATE, "xchunks: set before gossip_engine_connect_rccl");
         e->opt_xchunks = value;
     } else if (k == "rehearse_rows") {
         if (value < 0 || value > 64) return set_error(GOSSIP_EINVAL, "rehearse_rows: 0 (off) .. 64 row ranges");
