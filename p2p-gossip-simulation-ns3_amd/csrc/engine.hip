@@ -2300,10 +2300,13 @@ int gossip_engine::exchange_rccl(int64_t t) {
             }
             x_overflow_rounds++;
         }
-        for (uint32_t r = 0; r < R; r++) {  // capacities: 1.25x the largest count seen (rows)
-            uint64_t& cap = xcap[(size_t)r * kMaxChunks + c];
+        for (uint32_t r = 0; r < R; r++) {  // capacities: 1.25x the largest count seen (rows),
+            uint64_t& cap = xcap[(size_t)r * kMaxChunks + c];  // at most every tile row of the chunk
             const uint64_t tot = h_tot[(size_t)c * R + r];
-            if (tot > cap) cap = tot + tot / 4 + 16;
+            uint64_t rlo, rhi;
+            uint32_t rwl;
+            geom(r, c, &rlo, &rhi, &rwl);
+            if (tot > cap) cap = std::min<uint64_t>(tot + tot / 4 + 16, (rhi - rlo) * (hw / kTileWords));
         }
     }
     return GOSSIP_OK;
@@ -2714,9 +2717,13 @@ int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end
                         }
                         HIP_TRY(hipStreamSynchronize(e->stream));  // (receive buffers are reused)
                     }
-                    for (uint32_t r = 0; r < count; r++) {
+                    for (uint32_t r = 0; r < count; r++) {  // (at most every tile row of the chunk)
                         uint64_t& cap = e->xcap[(size_t)r * gossip_engine::kMaxChunks + c];
-                        if (tot[r] > cap) cap = tot[r] + tot[r] / 4 + 16;
+                        uint64_t lo, hi;
+                        uint32_t wl;
+                        geom(r, &lo, &hi, &wl);
+                        if (tot[r] > cap)
+                            cap = std::min<uint64_t>(tot[r] + tot[r] / 4 + 16, (hi - lo) * (e->hw / kTileWords));
                     }
                 }
             }
