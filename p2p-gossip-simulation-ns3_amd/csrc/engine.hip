@@ -755,6 +755,15 @@ gossip_engine::~gossip_engine() {
 }
 
 hipEvent_t gossip_engine::get_event() {
+    if (event_pool.empty()) {
+        // (created in batches, outside the launch sequence of a tick as far as possible: an event
+        // created between two launches of a timed phase delays the second one)
+        for (int k = 0; k < 64; k++) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) break;
+            event_pool.push_back(e);
+        }
+    }
     if (!event_pool.empty()) {
         hipEvent_t e = event_pool.back();
         event_pool.pop_back();
@@ -2428,6 +2437,12 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         HIP_TRY(hipSetDevice(e->device));
         HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
         HIP_TRY(hipDeviceGetAttribute(&e->num_cus, hipDeviceAttributeMultiprocessorCount, e->device));
+        if (cfg->flags & GOSSIP_F_TIMING)  // timed phases: no event creation inside a tick's launches
+            for (int k = 0; k < 256; k++) {
+                hipEvent_t ev = nullptr;
+                HIP_TRY(hipEventCreate(&ev));
+                e->event_pool.push_back(ev);
+            }
         e->L = cfg->latency_ns;
         e->t0 = cfg->t_start_ns;
         e->tick0 = cfg->t_start_ns / e->L;

@@ -15,3 +15,5 @@ for SR in "2 4" "2 8" "4 2"; do
 import json; d=json.loads(open('gpurun_out/r3_rows_s$1r$2.json').read().strip().splitlines()[-1])
 print('S=$1 R=$2', {k: (round(v,3) if isinstance(v,float) else v) for k,v in d.items() if k in ('rank_gpu_ms_per_tick_max','rank_ingress_bytes_per_tick_max','unpartitioned_pull_ms_per_tick','rank_device_gib','window_words')})"
 done
+timeout -k 10 300 python tools/bench_dense.py c2 --batch --modes dense > gpurun_out/r3r_dense_c2.json 2> gpurun_out/r3r_dense_c2.err || exit 1
+cat gpurun_out/r3r_dense_c2.json
