@@ -968,8 +968,9 @@ int gossip_engine::alloc_device() {
         const uint64_t lim = (uint64_t)opt_mem_limit > graph ? (uint64_t)opt_mem_limit - graph : 0ull;
         freeb = (size_t)std::min<uint64_t>(freeb, lim);
     }
-    if (cfg.max_words == 0 && row_count == 1) {
-        // (row-partitioned ranks skip this: their strides must agree for the row exchange)
+    if (cfg.max_words == 0 && row_count == 1 && opt_rehearse_rows <= 1) {
+        // (row-partitioned ranks skip this: their strides must agree for the row exchange; a row
+        // rehearsal leaves the memory to its exchange messages)
         // Headroom over the estimate: up to +25% (at least 2 tiles) of row capacity, as far as
         // device memory allows.  Unused capacity costs memory only -- the kernels touch the live
         // words [0, wact) of a row -- while a short estimate on a graph whose bitmaps fill the
