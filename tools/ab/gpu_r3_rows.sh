@@ -6,8 +6,10 @@ R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd $R
 A="--steps 20 --warmup 5 --no-cpu-baseline"
+if [ "${WITH_S8:-0}" = 1 ]; then
 timeout -k 10 420 python bench.py $A --rehearse-shards 8 > gpurun_out/r3_rows_s8.json 2> gpurun_out/r3_rows_s8.err || { tail -5 gpurun_out/r3_rows_s8.err; exit 1; }
 python tools/ab_line.py s8 gpurun_out/r3_rows_s8.json
+fi
 for SR in "2 4" "2 8" "4 2"; do
   set -- $SR
   timeout -k 10 420 python bench.py $A --rehearse-shards $1 --rehearse-rows $2 > gpurun_out/r3_rows_s$1r$2.json 2> gpurun_out/r3_rows_s$1r$2.err || { tail -5 gpurun_out/r3_rows_s$1r$2.err; exit 1; }
