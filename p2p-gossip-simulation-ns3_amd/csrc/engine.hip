@@ -1623,15 +1623,26 @@ int gossip_engine::tick_step_a(int64_t t) {
         };
         hipEvent_t e0 = nullptr, e1 = nullptr, p0 = nullptr, p1 = nullptr;
         a.inc = nullptr;
-        if (dense && (cfg.flags & GOSSIP_F_TIMING)) {  // DENSE phase: transpose + MFMA + dedup
-            p0 = get_event();
-            HIP_TRY(hipEventRecord(p0, stream));
-        }
+        // DENSE phase = transpose + MFMA + dedup, each kernel timed on its own (the phase is the
+        // sum: host-side gaps between the launches of a tick are not the kernels' time)
+        const bool dense_timing = dense && (cfg.flags & GOSSIP_F_TIMING);
+        auto phase_begin = [&]() -> hipEvent_t {
+            if (!dense_timing) return nullptr;
+            hipEvent_t x = get_event();
+            return hipEventRecord(x, stream) == hipSuccess ? x : nullptr;
+        };
+        auto phase_end = [&](hipEvent_t x) {
+            if (!x) return;
+            hipEvent_t y = get_event();
+            if (hipEventRecord(y, stream) == hipSuccess) timers_phase.emplace_back(x, y);
+        };
         if (dense) {  // transpose the frontier to share-column bit rows (not timed as the pull)
+            hipEvent_t q = phase_begin();
             dim3 eg(n_pad / 256u, wact);
             k_transpose<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad / 32u, wact, a.live_prev,
                                                 d_nz[fcur], ntw, d_FT);
             HIP_TRY(hipGetLastError());
+            phase_end(q);
         }
         // young tiles beside k_pull: the two kernels touch disjoint words; they share the per-node
         // counters and occupancy words, which k_pull then updates atomically (shared_out) into
@@ -1700,6 +1711,7 @@ int gossip_engine::tick_step_a(int64_t t) {
         // DENSE mode: dedup of the incoming words of rows [base.v0, base.n), one node per wave
         // step, the grid sized to the rows (k_dense_dedup, dense_kernel.h)
         auto run_dedup = [&](const PullArgs& base) {
+            hipEvent_t q = phase_begin();
             const uint64_t rows = base.n > base.v0 ? base.n - base.v0 : 0;
             const uint32_t g = (uint32_t)std::max<uint64_t>(
                 1, std::min<uint64_t>((rows + kDedupWaves - 1) / kDedupWaves, 2u * (uint32_t)num_cus));
@@ -1709,6 +1721,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 c.wact = std::min(kPullLdsWords, wact - wb);
                 k_dense_dedup<<<g, 64 * kDedupWaves, pull_lds_bytes(c.wact, c.keep_lds != 0), stream>>>(c);
             }
+            phase_end(q);
         };
         // the MFMA contraction of rows [lo, hi) (DENSE mode) into the incoming words
         auto run_dense = [&](uint64_t lo, uint64_t hi) -> int {
@@ -1724,8 +1737,10 @@ int gossip_engine::tick_step_a(int64_t t) {
             while ((uint64_t)gm.mb * gm.nt * ks < min_tiles && ks * 4 <= nst) ks *= 2;
             gm.ksplit = ks;
             gm.total = gm.mb * gm.nt * ks;
+            hipEvent_t q = phase_begin();
             k_dense_bits<<<(gm.total + 7u) / 8u * 8u, 512, 0, stream>>>(gm);
             HIP_TRY(hipGetLastError());
+            phase_end(q);
             return GOSSIP_OK;
         };
         if (nchunks > 1) {
@@ -1824,11 +1839,6 @@ int gossip_engine::tick_step_a(int64_t t) {
                 HIP_TRY(hipEventRecord(p1, stream));
                 timers_phase.emplace_back(p0, p1);
             }
-        }
-        if (dense && p0) {
-            p1 = get_event();
-            HIP_TRY(hipEventRecord(p1, stream));
-            timers_phase.emplace_back(p0, p1);
         }
         HIP_TRY(hipGetLastError());
         pull_launches++;

@@ -122,7 +122,8 @@ def main():
             out["dense_tiles_skipped"] = c.dense_tiles_skipped
             out["mfma_tops"] = c.dense_ops / (c.pull_ms * 1e-3) / 1e12 if c.pull_ms else None
             # kernel-only: k_dense_bits alone; phase: k_transpose + k_dense_bits + k_dense_dedup,
-            # HIP events around the three on the engine stream (the whole DENSE pull of a tick)
+            # each timed by HIP events around its own launch and summed (the whole DENSE pull of
+            # a tick, without the host-side gaps between the launches)
             out["mfma_util"] = c.dense_ops / (c.pull_ms * 1e-3) / INT8_PEAK_OPS if c.pull_ms else None
             out["phase_ms_total"] = c.pull_phase_ms
             out["phase_ms_avg"] = c.pull_phase_ms / max(c.pull_launches, 1)
