@@ -109,6 +109,12 @@ struct PullArgs {
     uint32_t shared_out = 0;
     uint32_t keep_lds = 0;  // some word of the launch has WF_KEEP: masks staged in LDS (k_pull)
     uint32_t gate_seen = 1;  // k_pull<LPW,1>: skip the own-seen loads of tiles no peer occupies
+    // Pass -> tile map (option pull_tiles): a k_pull pass covers LPW / 8 tiles taken from this
+    // list of launch-local tile indices (0xffff = padding) instead of LPW / 8 consecutive tiles,
+    // so passes skip tiles that hold nothing for k_pull (young, retired); every group of LPW / 8
+    // entries lies in one occupancy word.  Null: consecutive tiles.
+    const uint16_t* ptile = nullptr;
+    uint32_t nptile = 0;
 };
 
 // Phase-ordered update of id groups inside one word (rare: only words holding groups).
@@ -590,6 +596,12 @@ struct gossip_engine {
     int64_t opt_young_overlap = 1;    // k_pull_young beside k_pull on a second stream (1-4) or after (0)
     int64_t opt_young_grid = 0;       // k_pull_young blocks, 0 = the pull grid
     int64_t opt_pull_gate = 1;        // k_pull: occupancy-gated own-seen loads
+    int64_t opt_pull_tiles = 1;       // k_pull: passes over the listed (allocated, non-young) tiles only
+    // per staging slot: the pass -> tile lists of the tick's k_pull launches (PullArgs::ptile)
+    uint16_t* h_ptile[kRing] = {};
+    uint16_t* d_ptile[kRing] = {};
+    uint64_t ptile_cap = 0;
+    std::vector<uint32_t> pt_off, pt_cnt;  // per launch window of this tick
     int64_t opt_young_waves = 4;      // k_pull_young register budget: waves per SIMD (4, 5, 6)
     int64_t opt_late_age = -1;        // k_pull early exit for tiles >= this many ticks old (0: off, -1: auto)
     int64_t late_age_now() const {    // auto: every tile of a gathering (CSR) pull
@@ -724,6 +736,7 @@ gossip_engine::~gossip_engine() {
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     hipFree(d_msg); hipFree(d_cnt); hipFree(d_scan_tmp); hipFree(d_recv_msgs); hipFree(d_sizes);
     hipFree(d_tot); hipFree(d_ovf); hipHostFree(h_tot);
+    for (int k = 0; k < kRing; k++) { hipFree(d_ptile[k]); hipHostFree(h_ptile[k]); }
     hipFree(d_slot[0]); hipFree(d_slot[1]);
     hipFree(d_rev); hipFree(d_hint[0]); hipFree(d_hint[1]);
     for (int k = 0; k < kRing; k++) { hipFree(d_young[k]); hipHostFree(h_young[k]); }
@@ -1521,6 +1534,52 @@ int gossip_engine::tick_step_a(int64_t t) {
         if (YP->yt[i].flags)
             for (uint32_t q = 0; q < kTileWords; q++) WF[YP->yt[i].tile * kTileWords + q] |= (uint8_t)WF_YOUNG;
     for (uint32_t w : reset_now) ctl[w].clear = 0ull;
+    // 4b. k_pull's pass -> tile lists (option pull_tiles), one per launch window: the allocated,
+    //     non-young tiles, grouped by occupancy word and padded to whole passes of LPW / 8 tiles
+    //     (LPW as run_pull picks it below).  Young tiles are k_pull_young's, retired tiles hold
+    //     nothing; a pass then never spends its lanes on them.
+    pt_off.clear();
+    pt_cnt.clear();
+    const bool use_ptile = opt_pull_tiles && !dense && !(cfg.flags & (GOSSIP_F_NOSKIP | GOSSIP_F_WIDE_PULL)) && hw;
+    if (use_ptile) {
+        const uint64_t need = (uint64_t)hw / kTileWords + 16ull * ((hw + kPullLdsWords - 1) / kPullLdsWords) + 16;
+        if (need > ptile_cap) {
+            HIP_TRY(hipStreamSynchronize(stream));
+            for (int k = 0; k < kRing; k++) {
+                hipFree(d_ptile[k]);
+                hipHostFree(h_ptile[k]);
+                HIP_TRY(hipMalloc(&d_ptile[k], need * 2));
+                HIP_TRY(hipHostMalloc(&h_ptile[k], need * 2, hipHostMallocDefault));
+            }
+            ptile_cap = need;
+        }
+        uint16_t* P = h_ptile[slot];
+        uint32_t at = 0;
+        for (uint32_t wb = 0; wb < hw; wb += kPullLdsWords) {
+            const uint32_t wl = std::min(kPullLdsWords, hw - wb);
+            int lpw = 8;
+            while (lpw < 64 && 2 * lpw < (int)wl) lpw *= 2;
+            if (lpw == 64) lpw = pull_lanes_per_node(opt_pull_lpw);  // (run_pull: wide windows)
+            const uint32_t tpp = (uint32_t)lpw / 8u;
+            pt_off.push_back(at);
+            const uint32_t t0 = wb / kTileWords, t1 = (wb + wl) / kTileWords;
+            uint32_t group_tw = 0xffffffffu, in_group = 0;
+            for (uint32_t tl = t0; tl < t1; tl++) {
+                if (!tile_alloc[tl] || (WF[tl * kTileWords] & WF_YOUNG)) continue;
+                const uint32_t tw = tl >> 6;
+                if (tw != group_tw) {  // a pass never straddles two occupancy words
+                    while (in_group % tpp) { P[at++] = 0xffffu; in_group++; }
+                    group_tw = tw;
+                    in_group = 0;
+                }
+                P[at++] = (uint16_t)(tl - t0);
+                in_group++;
+            }
+            while (in_group % tpp) { P[at++] = 0xffffu; in_group++; }
+            pt_cnt.push_back(at - pt_off.back());
+        }
+        if (at) HIP_TRY(hipMemcpyAsync(d_ptile[slot], P, (size_t)at * 2, hipMemcpyHostToDevice, stream));
+    }
     // 5. upload + launches
     const uint32_t wact = hw;
     if (wact) HIP_TRY(hipMemcpyAsync(d_ctl[slot], C, (size_t)wact * sizeof(WordCtl), hipMemcpyHostToDevice, stream));
@@ -1600,10 +1659,14 @@ int gossip_engine::tick_step_a(int64_t t) {
         // (edge-lanes) when peers are many -- and never in DENSE mode, which gathers nothing.
         auto run_pull = [&](const PullArgs& base, bool split_edges) {
             const uint32_t grid = grid_for(base.v0, base.n);
-            for (uint32_t wb = 0; wb < wact; wb += kPullLdsWords) {
+            for (uint32_t wb = 0, li = 0; wb < wact; wb += kPullLdsWords, li++) {
                 PullArgs c = base;
                 c.wbase = wb;
                 c.wact = std::min(kPullLdsWords, wact - wb);
+                if (use_ptile && split_edges && li < pt_off.size()) {
+                    c.ptile = d_ptile[slot] + pt_off[li];
+                    c.nptile = pt_cnt[li];
+                }
                 int lpw = 8;
                 while (lpw < 64 && 2 * lpw < (int)c.wact) lpw *= 2;
                 // windows wider than 64 words keep one peer walk per node (the pipelined path)
@@ -1618,7 +1681,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 if (wide)
                     k_pull_wide<<<grid, 256, pull_lds_bytes(c.wact), stream>>>(c);
                 else
-                    launch_pull(lpw, epn, nt_rows, grid, pull_lds_bytes(c.wact, c.keep_lds != 0), stream, c);
+                    launch_pull(lpw, epn, nt_rows, grid, pull_lds_bytes(c.wact, c.keep_lds != 0, c.nptile), stream, c);
             }
         };
         hipEvent_t e0 = nullptr, e1 = nullptr, p0 = nullptr, p1 = nullptr;
@@ -1660,6 +1723,9 @@ int gossip_engine::tick_step_a(int64_t t) {
             }
             HIP_TRY(hipMemsetAsync(d_nz[nxt] + (uint64_t)v0 * ntw, 0, (size_t)(v1 - v0) * ntw * 8u, stream));
             a.shared_out = 1u;
+        } else if (use_ptile) {
+            // k_pull writes whole occupancy words only for the words its listed tiles fall in
+            HIP_TRY(hipMemsetAsync(d_nz[nxt] + (uint64_t)v0 * ntw, 0, (size_t)(v1 - v0) * ntw * 8u, stream));
         }
         if (cfg.flags & GOSSIP_F_TIMING) {
             e0 = get_event();
@@ -2472,6 +2538,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_young_overlap = env_option("GOSSIP_YOUNG_OVERLAP", 1);
         e->opt_young_grid = env_option("GOSSIP_YOUNG_GRID", 0);
         e->opt_pull_gate = env_option("GOSSIP_PULL_GATE", 1);
+        e->opt_pull_tiles = env_option("GOSSIP_PULL_TILES", 1);
         e->opt_young_waves = env_option("GOSSIP_YOUNG_WAVES", 4);
         e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
         e->opt_xchunks = env_option("GOSSIP_XCHUNKS", 4);
@@ -2792,6 +2859,9 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     } else if (k == "young_overlap") {
         if (value < 0 || value > 4) return set_error(GOSSIP_EINVAL, "young_overlap: 0 .. 4");
         e->opt_young_overlap = value;
+    } else if (k == "pull_tiles") {
+        if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "pull_tiles: 0 or 1");
+        e->opt_pull_tiles = value;
     } else if (k == "pull_gate") {
         if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "pull_gate: 0 or 1");
         e->opt_pull_gate = value;

@@ -81,9 +81,11 @@ __device__ __forceinline__ void store_row16(uint64_t* p, uint64_t x, uint64_t y)
 
 // + the keep masks of the launch's words when some word has WF_KEEP (the cut tick): read from
 // LDS, a flagged word's mask never makes the wave wait on a global load
-__host__ __device__ constexpr size_t pull_lds_bytes(uint32_t wact, bool keep = false) {
-    return (size_t)wact * 16u + (((size_t)wact + 15u) & ~(size_t)15u) + (keep ? (size_t)wact * 8u : 0u);
+__host__ __device__ constexpr size_t pull_lds_bytes(uint32_t wact, bool keep = false, uint32_t nptile = 0) {
+    return (size_t)wact * 16u + (((size_t)wact + 15u) & ~(size_t)15u) + (keep ? (size_t)wact * 8u : 0u) +
+           (((size_t)nptile * 2u + 15u) & ~(size_t)15u);
 }
+constexpr uint32_t kNoWord = 0xffffffffu;
 
 // Peer ids of the first GRP peers of item k's node (0xffffffff past the list).
 template <int LPW, int EPN>
@@ -117,6 +119,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     unsigned long long* s_new = smem + a.wact;   // liveness of this tick (OR of new bits)
     uint8_t* s_wf = reinterpret_cast<uint8_t*>(smem + 2u * a.wact);
     unsigned long long* s_keep = smem + 2u * a.wact + ((a.wact + 15u) & ~15u) / 8u;
+    uint16_t* s_pt = reinterpret_cast<uint16_t*>(s_keep + (a.keep_lds ? a.wact : 0u));
     for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
         const uint8_t f = a.wflags[a.wbase + i];
         // a young word is k_pull_young's: dead here, no clear, no write
@@ -125,6 +128,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
         s_wf[i] = (f & WF_YOUNG) ? (uint8_t)0 : f;
         if (a.keep_lds) s_keep[i] = (f & WF_KEEP) ? a.ctl[a.wbase + i].keep : ~0ull;
     }
+    for (uint32_t i = threadIdx.x; i < a.nptile; i += 256) s_pt[i] = a.ptile[i];
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane % GRP, wl = gl % LPW, el = gl / LPW, slot = lane / GRP;
@@ -132,23 +136,50 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     const uint64_t n = a.n;
     const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
-    const uint32_t npass = (a.wact + 2u * LPW - 1u) / (2u * LPW);
+    // Pass geometry: consecutive 2 LPW-word passes, or (pull_tiles) LPW / 8 listed tiles per pass
+    constexpr uint32_t TPP = LPW >= 8 ? (uint32_t)LPW / 8u : 1u;
+    const bool listed = a.ptile != nullptr;
+    const uint32_t npass = listed ? a.nptile / TPP : (a.wact + 2u * LPW - 1u) / (2u * LPW);
+    // launch-local word of this lane's pair in pass p (kNoWord: none)
+    auto lw_of = [&](uint32_t p) -> uint32_t {
+        if (!listed) {
+            const uint32_t x = p * 2u * LPW + 2u * wl;
+            return x < a.wact ? x : kNoWord;
+        }
+        const uint32_t t = s_pt[p * TPP + (wl >> 3)];
+        return t == 0xffffu ? kNoWord : t * 16u + 2u * (wl & 7u);
+    };
+    // the occupancy word (1,024 words) of pass p: one per pass (listed groups never straddle one)
+    auto tw_of = [&](uint32_t p) -> uint32_t {
+        return listed ? (a.wbase + (uint32_t)s_pt[p * TPP] * 16u) >> 10 : (a.wbase + p * 2u * LPW) >> 10;
+    };
+    // bit k = the occupancy bit of pass p's k-th tile in the nz word nzw (a peer's, of tw_of(p))
+    auto pass_bits = [&](unsigned long long nzw, uint32_t p) -> uint32_t {
+        if (!listed) return (uint32_t)(nzw >> (((a.wbase + p * 2u * LPW) >> 4) & 63u)) & 0xffu;
+        uint32_t r = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < TPP; k++) {
+            const uint32_t t = s_pt[p * TPP + k];
+            if (t != 0xffffu) r |= (uint32_t)((nzw >> (((a.wbase >> 4) + t) & 63u)) & 1ull) << k;
+        }
+        return r;
+    };
     const uint32_t nsteps = 64u / NPW;
     unsigned long long snap_local = 0ull;
     uint32_t t_pe = 0, t_col = 0, t_srd = 0, t_swr = 0, t_fwr = 0, t_nz = 0;  // wave-uniform
     unsigned long long nzacc = 0ull;
     const bool gather = a.inc == nullptr && EPN == 1;  // the pipelined id/occupancy loads
 
-    for (uint64_t c0 = a.v0 + wave * 64u; c0 < n; c0 += nwaves * 64u) {
+    for (uint64_t c0 = a.v0 + wave * 64u; npass && c0 < n; c0 += nwaves * 64u) {
         const int64_t rp = a.rowptr[min(c0 + lane, n)];
         const int64_t rp_end = a.rowptr[min(c0 + 64u, n)];
-        // item k = (step, pass): node c0 + step * NPW + slot, words wbase + pass * 2 LPW + 2 wl
+        // item k = (step, pass): node c0 + step * NPW + slot, the lane's word pair lw_of(pass)
         uint32_t step = 0, pass = 0;
         ulonglong2 s2c = make_ulonglong2(0ull, 0ull);
         {
             const uint64_t v = c0 + slot;
-            const uint32_t lw = 2u * wl;
-            if (v < n && lw < a.wact && (s_lp[lw] | s_lp[lw + 1u]) != 0ull)
+            const uint32_t lw = lw_of(0u);
+            if (v < n && lw != kNoWord && (s_lp[lw] | s_lp[lw + 1u]) != 0ull)
                 s2c = load_row16<NT>(a.seen + v * stride + a.wbase + lw);
         }
         uint32_t cid0 = 0xffffffffu, cid1 = 0xffffffffu;
@@ -156,7 +187,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
         if (gather) {
             cid0 = pull_cid_load<LPW, EPN>(a, 0u, c0, rp, rp_end, gl, slot);
             cid1 = npass > 1u ? cid0 : pull_cid_load<LPW, EPN>(a, 1u, c0, rp, rp_end, gl, slot);
-            nz0 = cid0 != 0xffffffffu ? a.nz_cur[(uint64_t)cid0 * a.ntw + (a.wbase >> 10)] : 0ull;
+            nz0 = cid0 != 0xffffffffu ? a.nz_cur[(uint64_t)cid0 * a.ntw + tw_of(0u)] : 0ull;
             t_nz += wave_count(cid0 != 0xffffffffu);
         }
         uint32_t cnt = 0;
@@ -179,8 +210,10 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             const uint32_t step2 = pass1 + 1u < npass ? step1 : step1 + 1u;
             const uint32_t idx = step * NPW + slot;
             const uint32_t v = (uint32_t)(c0 + idx);
-            const uint32_t w = a.wbase + pass * 2u * LPW + 2u * wl;
-            const bool act = c0 + idx < n && w < a.wbase + a.wact;
+            const uint32_t lw0 = lw_of(pass);
+            const uint32_t w = a.wbase + (lw0 == kNoWord ? 0u : lw0);
+            const bool act = c0 + idx < n && lw0 != kNoWord;
+            const uint32_t tw = tw_of(pass);  // (uniform: the pass's occupancy word)
             // ---- stage loads: own seen pair of item k+1, ids of k+2, occupancy of k+1 ----
             ulonglong2 s2n = make_ulonglong2(0ull, 0ull);
             bool s2n_gated = false;
@@ -194,7 +227,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             if (step1 < nsteps) {
                 // (a dead pair's seen words are never needed: only cleared, never merged)
                 const uint64_t v1 = c0 + step1 * NPW + slot;
-                const uint32_t lw1 = pass1 * 2u * LPW + 2u * wl;
+                const uint32_t lw1 = lw_of(pass1);
                 // this item's peer range, read with the whole wave active: a shuffle inside the
                 // branch below would read the row pointers of lanes whose own pair is dead
                 // (inactive lanes give no data), so a node with more peers than one lane group
@@ -202,10 +235,9 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                 const uint32_t ix = step * NPW + slot;
                 const int32_t b0 = __shfl((int)rp, (int)ix, 64);
                 const int32_t e0 = ix + 1u < 64u ? __shfl((int)rp, (int)((ix + 1u) & 63u), 64) : (int32_t)rp_end;
-                if (v1 < n && lw1 < a.wact && (s_lp[lw1] | s_lp[lw1 + 1u]) != 0ull) {
+                if (v1 < n && lw1 != kNoWord && (s_lp[lw1] | s_lp[lw1 + 1u]) != 0ull) {
                     // same node and occupancy word as this item, peers in one lane group
-                    s2n_gated = gate && step1 == step &&
-                                ((a.wbase + lw1) >> 10) == ((a.wbase + pass * 2u * LPW) >> 10) && e0 - b0 <= GRP &&
+                    s2n_gated = gate && step1 == step && tw_of(pass1) == tw && e0 - b0 <= GRP &&
                                 !((nzor >> (((a.wbase + lw1) >> 4) & 63u)) & 1ull);
                     if (!s2n_gated) s2n = load_row16<NT>(a.seen + v1 * stride + a.wbase + lw1);
                 }
@@ -216,9 +248,8 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                 if (step2 < nsteps)
                     cid2 = step2 == step1 ? cid1 : pull_cid_load<LPW, EPN>(a, step2, c0, rp, rp_end, gl, slot);
                 if (step1 < nsteps) {
-                    const uint32_t tw1 = (a.wbase + pass1 * 2u * LPW) >> 10;
-                    const uint32_t tw0 = (a.wbase + pass * 2u * LPW) >> 10;
-                    if (step1 == step && tw1 == tw0) {
+                    const uint32_t tw1 = tw_of(pass1);
+                    if (step1 == step && tw1 == tw) {
                         nz1 = nz0;  // same node, same occupancy word
                     } else {
                         nz1 = cid1 != 0xffffffffu ? a.nz_cur[(uint64_t)cid1 * a.ntw + tw1] : 0ull;
@@ -259,7 +290,6 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
 #pragma unroll
             for (int off = GRP / 2; off > 4; off >>= 1) gneed |= __shfl_xor(gneed, off, GRP);
             // ---- gather peer rows ----
-            const uint32_t tw = w >> 10;  // one occupancy word per pass: a pass spans <= 8 tiles of 64
             const unsigned long long tbit = 1ull << ((w >> 4) & 63u);
             const int32_t beg = __shfl((int)rp, (int)idx, 64);
             const int32_t nxb = __shfl((int)rp, (int)((idx + 1u) & 63u), 64);
@@ -289,7 +319,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                     auto gchunk = [&](uint32_t cid, unsigned long long nzw, int rem) {
                         t_col += wave_count((int)gl < rem);
                         // the <= 8 occupancy bits of this pass's tiles, tested per lane by tile
-                        const uint32_t nzp = (uint32_t)(nzw >> ((((w - 2u * wl) >> 4)) & 63u)) & 0xffu;
+                        const uint32_t nzp = pass_bits(nzw, pass);
                         for (int t0 = 0; t0 < rem; t0 += kInflight) {
                             int open = (a.noskip || !late)
                                            ? 1 : (((want0 & ~acc0) | (want1 & ~acc1)) != 0ull);
@@ -421,7 +451,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
 #pragma unroll
                 for (int off = GRP / 2; off > 0; off >>= 1) nb |= __shfl_xor(nb, off, GRP);
                 nzacc |= nb;
-                const bool last_of_tw = pass + 1u == npass || ((a.wbase + (pass + 1u) * 2u * LPW) >> 10) != tw;
+                const bool last_of_tw = pass + 1u == npass || tw_of(pass + 1u) != tw;
                 if (last_of_tw) {
                     if (gl == 0 && c0 + idx < n) {
                         if (!a.shared_out)
@@ -453,7 +483,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             s2c_gated = s2n_gated;
             cid0 = cid1;
             cid1 = cid2;
-            nz_new = step1 != step || ((a.wbase + pass1 * 2u * LPW) >> 10) != ((a.wbase + pass * 2u * LPW) >> 10);
+            nz_new = step1 != step || tw_of(pass1) != tw;
             nz0 = nz1;
             step = step1;
             pass = pass1;
