@@ -46,6 +46,31 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 // Lanes of the wave for which c holds (a wave-uniform value: traffic accounting in SGPRs).
 __device__ __forceinline__ uint32_t wave_count(bool c) { return (uint32_t)__popcll(__ballot(c)); }
 
+// OR over aligned groups of G lanes.  Up to 16 lanes with DPP moves -- quad permutes, then the
+// row half-mirror (lane i <-> 7 - i of each 8) and the row mirror (i <-> 15 - i of each 16) -- which
+// are VALU operations; a __shfl_xor is a ds_bpermute through the LDS crossbar with a round trip
+// per step, and k_pull runs several of these reductions per work item.  Beyond 16 lanes the last
+// steps are shuffles.  Every lane of a group must be active (group-uniform control flow).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_or_step(uint32_t x) {
+    return x | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+template <int G>
+__device__ __forceinline__ uint32_t group_or(uint32_t x) {
+    static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "group size");
+    if constexpr (G >= 2) x = dpp_or_step<0xB1>(x);   // quad_perm [1,0,3,2]: lane ^ 1
+    if constexpr (G >= 4) x = dpp_or_step<0x4E>(x);   // quad_perm [2,3,0,1]: lane ^ 2
+    if constexpr (G >= 8) x = dpp_or_step<0x141>(x);  // row_half_mirror: the other quad of the 8
+    if constexpr (G >= 16) x = dpp_or_step<0x140>(x); // row_mirror: the other 8 of the row
+    if constexpr (G >= 32) x |= (uint32_t)__shfl_xor((int)x, 16, 64);
+    if constexpr (G >= 64) x |= (uint32_t)__shfl_xor((int)x, 32, 64);
+    return x;
+}
+template <int G>
+__device__ __forceinline__ unsigned long long group_or64(unsigned long long x) {
+    return (unsigned long long)group_or<G>((uint32_t)x) | ((unsigned long long)group_or<G>((uint32_t)(x >> 32)) << 32);
+}
+
 // WF_YOUNG: the word belongs to a young tile, which k_pull_young owns this tick (young_kernel.h)
 // WF_LATE: the word's tile is old enough (option late_age) for the bottom-up early exit
 enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u, WF_YOUNG = 16u, WF_LATE = 32u };
@@ -198,6 +223,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
         // same node and occupancy word (whose nz word is already in registers).
         unsigned long long nzor = 0ull;
         bool nz_new = true, s2c_gated = false;
+        int32_t beg = 0, end = 0;  // the current node's peer range (read once per node)
         const bool gate = gather && !a.noskip && a.gate_seen;
         // the first item's loads have landed before the item loop: inside it, every load is
         // then waited for by the item that issued it or the next (a loop header that merged a
@@ -213,14 +239,18 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             const uint32_t lw0 = lw_of(pass);
             const uint32_t w = a.wbase + (lw0 == kNoWord ? 0u : lw0);
             const bool act = c0 + idx < n && lw0 != kNoWord;
+            if (pass == 0u) {  // (uniform) a new node: its peer range, with the whole wave active
+                beg = __shfl((int)rp, (int)idx, 64);
+                const int32_t nxb = __shfl((int)rp, (int)((idx + 1u) & 63u), 64);
+                end = (idx + 1u < 64u) ? nxb : (int32_t)rp_end;
+            }
             const uint32_t tw = tw_of(pass);  // (uniform: the pass's occupancy word)
             // ---- stage loads: own seen pair of item k+1, ids of k+2, occupancy of k+1 ----
             ulonglong2 s2n = make_ulonglong2(0ull, 0ull);
             bool s2n_gated = false;
             if (gate && nz_new) {  // (uniform) this item starts a new occupancy word
                 unsigned long long x = nz0;
-#pragma unroll
-                for (int off = GRP / 2; off > 0; off >>= 1) x |= __shfl_xor(x, off, GRP);
+                x = group_or64<GRP>(x);
                 nzor = x;
                 nz_new = false;
             }
@@ -228,13 +258,11 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                 // (a dead pair's seen words are never needed: only cleared, never merged)
                 const uint64_t v1 = c0 + step1 * NPW + slot;
                 const uint32_t lw1 = lw_of(pass1);
-                // this item's peer range, read with the whole wave active: a shuffle inside the
-                // branch below would read the row pointers of lanes whose own pair is dead
-                // (inactive lanes give no data), so a node with more peers than one lane group
-                // could pass the one-group test below and be gated on a partial occupancy OR
-                const uint32_t ix = step * NPW + slot;
-                const int32_t b0 = __shfl((int)rp, (int)ix, 64);
-                const int32_t e0 = ix + 1u < 64u ? __shfl((int)rp, (int)((ix + 1u) & 63u), 64) : (int32_t)rp_end;
+                // this item's peer range was read with the whole wave active (a shuffle inside
+                // the branch below would read the row pointers of lanes whose own pair is dead --
+                // inactive lanes give no data -- so a node with more peers than one lane group
+                // could pass the one-group test below and be gated on a partial occupancy OR)
+                const int32_t b0 = beg, e0 = end;  // (this item's node)
                 if (v1 < n && lw1 != kNoWord && (s_lp[lw1] | s_lp[lw1 + 1u]) != 0ull) {
                     // same node and occupancy word as this item, peers in one lane group
                     s2n_gated = gate && step1 == step && tw_of(pass1) == tw && e0 - b0 <= GRP &&
@@ -282,18 +310,12 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             // read decision is made per tile: the 8 word-lanes of a tile load together and every
             // fetched line is fully used.
             int tn = need ? 1 : 0;
-            tn |= __shfl_xor(tn, 1, GRP);
-            tn |= __shfl_xor(tn, 2, GRP);
-            tn |= __shfl_xor(tn, 4, GRP);
+            tn = (int)group_or<8>((uint32_t)tn);  // per tile (8 word-lanes)
             const bool tneed = tn != 0 && act;
             int gneed = tn;
-#pragma unroll
-            for (int off = GRP / 2; off > 4; off >>= 1) gneed |= __shfl_xor(gneed, off, GRP);
+            gneed = (int)group_or<GRP>((uint32_t)gneed);
             // ---- gather peer rows ----
             const unsigned long long tbit = 1ull << ((w >> 4) & 63u);
-            const int32_t beg = __shfl((int)rp, (int)idx, 64);
-            const int32_t nxb = __shfl((int)rp, (int)((idx + 1u) & 63u), 64);
-            const int32_t end = (idx + 1u < 64u) ? nxb : (int32_t)rp_end;
             uint64_t acc0 = 0ull, acc1 = 0ull;
             if (a.inc) {
                 // DENSE mode: the gather already happened as an MFMA contraction; take the
@@ -323,12 +345,9 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                         for (int t0 = 0; t0 < rem; t0 += kInflight) {
                             int open = (a.noskip || !late)
                                            ? 1 : (((want0 & ~acc0) | (want1 & ~acc1)) != 0ull);
-                            open |= __shfl_xor(open, 1, GRP);  // per tile (8 word-lanes)
-                            open |= __shfl_xor(open, 2, GRP);
-                            open |= __shfl_xor(open, 4, GRP);
+                            open = (int)group_or<8>((uint32_t)open);  // per tile (8 word-lanes)
                             int gopen = open;
-#pragma unroll
-                            for (int off = GRP / 2; off > 4; off >>= 1) gopen |= __shfl_xor(gopen, off, GRP);
+                            gopen = (int)group_or<GRP>((uint32_t)gopen);
                             if (!gopen) break;  // uniform inside the node group
                             uint32_t u[kInflight], z[kInflight];
 #pragma unroll
@@ -415,9 +434,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             // (NOSKIP diagnostic: every tile row is written and marked occupied, so the pull
             // reads every peer row -- the dense-pull byte count)
             int ta = (n0 | n1) != 0ull || (a.noskip && act);
-            ta |= __shfl_xor(ta, 1, GRP);
-            ta |= __shfl_xor(ta, 2, GRP);
-            ta |= __shfl_xor(ta, 4, GRP);
+            ta = (int)group_or<8>((uint32_t)ta);
             // ---- state, counters (one lane per word pair) ----
             const bool own = act && el == 0;
             const bool swr = own && (dead ? ((f0 | f1) & WF_CLEAR) != 0u
@@ -448,8 +465,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             // ---- occupancy word of this node, written whole once per nz word index ----
             {
                 unsigned long long nb = (ta && own && (wl & 7u) == 0u) ? tbit : 0ull;
-#pragma unroll
-                for (int off = GRP / 2; off > 0; off >>= 1) nb |= __shfl_xor(nb, off, GRP);
+                nb = group_or64<GRP>(nb);
                 nzacc |= nb;
                 const bool last_of_tw = pass + 1u == npass || tw_of(pass + 1u) != tw;
                 if (last_of_tw) {
