@@ -187,6 +187,7 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
         acc["dev_bytes"] = max(acc["dev_bytes"], c1.device_bytes)
         acc["nt"], acc["grid"] = c1.pull_nt, c1.pull_grid
         acc["late_age"] = c1.pull_late_age
+        acc["pull_tiles"] = c1.pull_tiles
         acc["ramp_ticks"] = c0.ticks
         if rank == 0:
             log(f"[bench] shard {s} of {shards}: {c1.edge_events - c0.edge_events} edge events in "
@@ -439,7 +440,7 @@ def main():
         }
         variant = {"nt_rows": acc["nt"], "grid": acc["grid"],
                    "young_overlap": YOUNG_OVERLAP if acc["young_launches"] else None,
-                   "late_age": acc.get("late_age", 0)}
+                   "late_age": acc.get("late_age", 0), "pull_tiles": acc.get("pull_tiles", 0)}
         t_pull, why_pull = pmc_traffic(wl["name"], out, variant)
         k_pull["traffic"] = t_pull
         young = None

@@ -602,6 +602,7 @@ struct gossip_engine {
     uint16_t* d_ptile[kRing] = {};
     uint64_t ptile_cap = 0;
     std::vector<uint32_t> pt_off, pt_cnt;  // per launch window of this tick
+    bool pt_used = false;                  // the last tick's k_pull ran over tile lists
     int64_t opt_young_waves = 4;      // k_pull_young register budget: waves per SIMD (4, 5, 6)
     int64_t opt_late_age = -1;        // k_pull early exit for tiles >= this many ticks old (0: off, -1: auto)
     int64_t late_age_now() const {    // auto: every tile of a gathering (CSR) pull
@@ -1541,6 +1542,7 @@ int gossip_engine::tick_step_a(int64_t t) {
     pt_off.clear();
     pt_cnt.clear();
     const bool use_ptile = opt_pull_tiles && !dense && !(cfg.flags & (GOSSIP_F_NOSKIP | GOSSIP_F_WIDE_PULL)) && hw;
+    pt_used = use_ptile;
     if (use_ptile) {
         const uint64_t need = (uint64_t)hw / kTileWords + 16ull * ((hw + kPullLdsWords - 1) / kPullLdsWords) + 16;
         if (need > ptile_cap) {
@@ -3332,6 +3334,7 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     // and launch
     c->young_line2_misses = acct[15];
     c->pull_late_age = (uint32_t)e->late_age_now();
+    c->pull_tiles = e->pt_used ? 1u : 0u;
     c->young_bytes_moved = 128ull * (acct[8] + acct[10] + acct[13] + acct[14] + acct[15]) + 5ull * acct[9] +
                            8ull * (acct[11] + acct[12]) + e->young_launches * (8ull * (e->n + 1) + 16ull * e->n);
     uint64_t g = 0;
