@@ -262,6 +262,8 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *                      16 GiB), 0 / 1 forced                              [GOSSIP_PULL_NT]
  *   "pull_grid"        blocks per pull launch, 0 = auto (16,384 non-temporal, else 2,048)
  *                                                                         [GOSSIP_PULL_GRID]
+ *   "pull_tile_order"  1: k_pull's tile lists in age order inside each occupancy word (default),
+ *                      0: in tile order                                [GOSSIP_PULL_TILE_ORDER]
  *   "pull_lpw"         word-lanes per node for windows > 64 words: 0 auto (32), 16, 32, 64
  *                                                                         [GOSSIP_PULL_LPW]
  *   "dense_min_tiles"  MFMA block tiles the K split aims for (512)  [GOSSIP_DENSE_MIN_TILES]
@@ -276,6 +278,10 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *   "young_grid"       k_pull_young blocks, 0 = the pull grid                [GOSSIP_YOUNG_GRID]
  *   "young_waves"      k_pull_young register budget in waves per SIMD: 4 (no spills), 5, 6
  *                                                                         [GOSSIP_YOUNG_WAVES]
+ *   "young_own"        1: k_pull_young dedups a node's incoming bits against its own frontier
+ *                      of the last two ticks (its own slots, read with the peers'), reading
+ *                      seen only for id-group words and overflowed nodes; 0: against its seen
+ *                      words (default: measured faster on C4)                 [GOSSIP_YOUNG_OWN]
  *   "young_overlap"    0: k_pull_young after k_pull on the engine stream; 1: the two run
  *                      concurrently on two streams, k_pull_young launched first (default);
  *                      2: concurrently, k_pull launched first; 3 / 4: as 1 with the second

@@ -458,6 +458,7 @@ struct YoungPack {
     YoungTile yt[kYoungMax];  // k_pull_young's tiles, sorted by tile
     uint32_t wt[64];          // write-sparse index -> tile (births, spills)
     uint8_t lv[kYoungMax];    // positions in yt of the leaving tiles, by tile
+    uint8_t map2[64];         // t-2's write index -> read position of the same tile (0xff: none)
 };
 
 constexpr int kRing = 4;   // host staging slots
@@ -597,6 +598,7 @@ struct gossip_engine {
     int64_t opt_young_grid = 0;       // k_pull_young blocks, 0 = the pull grid
     int64_t opt_pull_gate = 1;        // k_pull: occupancy-gated own-seen loads
     int64_t opt_pull_tiles = 1;       // k_pull: passes over the listed (allocated, non-young) tiles only
+    int64_t opt_pull_tile_order = 1;  // ... listed in age order within an occupancy word
     // per staging slot: the pass -> tile lists of the tick's k_pull launches (PullArgs::ptile)
     uint16_t* h_ptile[kRing] = {};
     uint16_t* d_ptile[kRing] = {};
@@ -604,6 +606,7 @@ struct gossip_engine {
     std::vector<uint32_t> pt_off, pt_cnt;  // per launch window of this tick
     bool pt_used = false;                  // the last tick's k_pull ran over tile lists
     int64_t opt_young_waves = 4;      // k_pull_young register budget: waves per SIMD (4, 5, 6)
+    int64_t opt_young_own = 0;        // k_pull_young dedups against the node's own last two frontiers
     int64_t opt_late_age = -1;        // k_pull early exit for tiles >= this many ticks old (0: off, -1: auto)
     int64_t late_age_now() const {    // auto: every tile of a gathering (CSR) pull
         return opt_late_age >= 0 ? opt_late_age : dense ? 0 : kAutoLateAge;
@@ -622,6 +625,7 @@ struct gossip_engine {
     std::vector<int64_t> tile_first;           // tick of a tile's first birth
     std::vector<uint8_t> tile_widx;            // write-sparse index of the last tick (0xff: none)
     std::vector<uint32_t> wt_last;             // write-sparse index -> tile of the last tick
+    std::vector<uint32_t> wt_last2;            // ... and of the tick before (own-frontier dedup)
     YoungPack* h_young[kRing] = {};
     YoungPack* d_young[kRing] = {};
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers_young;
@@ -1448,6 +1452,12 @@ int gossip_engine::tick_step_a(int64_t t) {
         for (uint32_t r = 0; r < ny_read; r++)
             if (YP->yt[r].flags == YT_READ) YP->lv[ny_leave++] = (uint8_t)r;
         std::sort(YP->lv, YP->lv + ny_leave, [&](uint8_t a, uint8_t b) { return YP->yt[a].tile < YP->yt[b].tile; });
+        // own-frontier dedup (young_kernel.h): where each tile of t-2's write list sits among this
+        // tick's read tiles (the same allocation: a young tile never retires while young)
+        std::memset(YP->map2, 0xff, sizeof(YP->map2));
+        for (uint32_t i = 0; i < wt_last2.size() && i < 64; i++)
+            for (uint32_t r = 0; r < ny_read; r++)
+                if (wt_last[r] == wt_last2[i] && tile_first[wt_last[r]] + 2 <= t) YP->map2[i] = (uint8_t)r;
         for (uint32_t q = 0; q < nb; q++) {
             const uint32_t tl = B[q].col >> 10;
             B[q].widx = tl < new_widx.size() ? new_widx[tl] : 0xffu;
@@ -1565,19 +1575,28 @@ int gossip_engine::tick_step_a(int64_t t) {
             const uint32_t tpp = (uint32_t)lpw / 8u;
             pt_off.push_back(at);
             const uint32_t t0 = wb / kTileWords, t1 = (wb + wl) / kTileWords;
-            uint32_t group_tw = 0xffffffffu, in_group = 0;
+            // per occupancy word, the tiles in age order (option pull_tile_order): a pass's tiles
+            // then reach their early exit (late_age) after similar numbers of peer batches, so
+            // fewer lanes idle while the wave finishes the pass's slowest tile
+            std::vector<uint32_t> grp;
+            auto flush = [&]() {
+                if (opt_pull_tile_order)
+                    std::stable_sort(grp.begin(), grp.end(), [&](uint32_t x, uint32_t y) { return tile_first[x] < tile_first[y]; });
+                for (uint32_t tl : grp) P[at++] = (uint16_t)(tl - t0);
+                for (size_t k = grp.size(); k % tpp; k++) P[at++] = 0xffffu;
+                grp.clear();
+            };
+            uint32_t group_tw = 0xffffffffu;
             for (uint32_t tl = t0; tl < t1; tl++) {
                 if (!tile_alloc[tl] || (WF[tl * kTileWords] & WF_YOUNG)) continue;
                 const uint32_t tw = tl >> 6;
                 if (tw != group_tw) {  // a pass never straddles two occupancy words
-                    while (in_group % tpp) { P[at++] = 0xffffu; in_group++; }
+                    flush();
                     group_tw = tw;
-                    in_group = 0;
                 }
-                P[at++] = (uint16_t)(tl - t0);
-                in_group++;
+                grp.push_back(tl);
             }
-            while (in_group % tpp) { P[at++] = 0xffffu; in_group++; }
+            flush();
             pt_cnt.push_back(at - pt_off.back());
         }
         if (at) HIP_TRY(hipMemcpyAsync(d_ptile[slot], P, (size_t)at * 2, hipMemcpyHostToDevice, stream));
@@ -1752,6 +1771,9 @@ int gossip_engine::tick_step_a(int64_t t) {
             y.cap = (uint32_t)std::min<int64_t>(kSlotU16 - 1, std::max<int64_t>(1, opt_young_cap));
             y.hint_cur = d_hint[fcur]; y.hint_next = d_hint[nxt]; y.rev = d_rev;
             y.stamp_cur = hint_stamp(t - 1); y.stamp_next = hint_stamp(t);
+            y.map2 = d_young[slot]->map2;
+            y.own = (opt_young_own && ny_read) ? 1u : 0u;
+            y.n2 = y.own ? (uint32_t)std::min<size_t>(wt_last2.size(), 64) : 0u;
             const uint32_t yg = (uint32_t)std::max<uint64_t>(
                 1, std::min<uint64_t>(((uint64_t)(v1 - v0) + 3) / 4,
                                       opt_young_grid > 0 ? (uint64_t)opt_young_grid : pull_grid_cap(nt_rows, opt_pull_grid)));
@@ -1921,6 +1943,7 @@ int gossip_engine::tick_step_a(int64_t t) {
     }
     if (young) {  // F_next's slots hold this tick's write-sparse tiles: next tick reads them
         tile_widx.swap(new_widx);
+        wt_last2.swap(wt_last);
         wt_last.assign(YP->wt, YP->wt + nwt);
     }
     if (smask_any) {  // hop-batched snapshots: arrivals of this tick that precede each snapshot
@@ -2541,7 +2564,9 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_young_grid = env_option("GOSSIP_YOUNG_GRID", 0);
         e->opt_pull_gate = env_option("GOSSIP_PULL_GATE", 1);
         e->opt_pull_tiles = env_option("GOSSIP_PULL_TILES", 1);
+        e->opt_pull_tile_order = env_option("GOSSIP_PULL_TILE_ORDER", 1);
         e->opt_young_waves = env_option("GOSSIP_YOUNG_WAVES", 4);
+        e->opt_young_own = env_option("GOSSIP_YOUNG_OWN", 0);
         e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
         e->opt_xchunks = env_option("GOSSIP_XCHUNKS", 4);
         e->opt_late_age = env_option("GOSSIP_LATE_AGE", -1);
@@ -2861,12 +2886,18 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     } else if (k == "young_overlap") {
         if (value < 0 || value > 4) return set_error(GOSSIP_EINVAL, "young_overlap: 0 .. 4");
         e->opt_young_overlap = value;
+    } else if (k == "pull_tile_order") {
+        if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "pull_tile_order: 0 or 1");
+        e->opt_pull_tile_order = value;
     } else if (k == "pull_tiles") {
         if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "pull_tiles: 0 or 1");
         e->opt_pull_tiles = value;
     } else if (k == "pull_gate") {
         if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "pull_gate: 0 or 1");
         e->opt_pull_gate = value;
+    } else if (k == "young_own") {
+        if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "young_own: 0 or 1");
+        e->opt_young_own = value;
     } else if (k == "young_waves") {
         if (value < 4 || value > 6) return set_error(GOSSIP_EINVAL, "young_waves: 4, 5 or 6");
         e->opt_young_waves = value;

@@ -87,6 +87,13 @@ struct YoungArgs {
     uint8_t* hint_next;
     const int32_t* rev;
     uint32_t stamp_cur, stamp_next;
+    // Own-frontier dedup (option young_own): a node's processed bits among its incoming ones are
+    // exactly its own frontier bits of the last two ticks (see k_pull_young), read from its own
+    // slots -- F_{t-1} in slot_cur, F_{t-2} in slot_next before this tick overwrites it -- in the
+    // same round trip as the peers' slots.  map2[w] = the read position of the tile whose t-2
+    // write index was w (0xff: none); n2 = entries of t-2's write list (0: slot_next is stale).
+    const uint8_t* map2;
+    uint32_t own, n2;
 };
 
 constexpr uint32_t kYoungSpare = 32;  // spare accumulator words per wave (tombstones land here)
@@ -95,7 +102,7 @@ __host__ __device__ constexpr size_t young_lds_bytes(uint32_t ny, uint32_t nr) {
     // 4 waves x (accumulator 8 B per read word + spares, touched list 2 B per read word, a slot
     // staging buffer), tiles, read-word flags, leaving positions
     return 4u * ((size_t)nr * 16u + kYoungSpare) * 8u + 4u * (size_t)nr * 16u * 2u + 4u * kSlotU16 * 2u +
-           (size_t)ny * sizeof(YoungTile) + (size_t)nr * 16u + 64u;
+           (size_t)ny * sizeof(YoungTile) + (size_t)nr * 16u + 64u + 64u;
 }
 
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane) {
@@ -131,8 +138,10 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
     YoungTile* s_yt = reinterpret_cast<YoungTile*>(reinterpret_cast<uint16_t*>(smem + 4u * accw) + 4u * nrw + 4u * kSlotU16);
     uint8_t* s_wf = reinterpret_cast<uint8_t*>(s_yt + a.ny);
     uint8_t* s_lv = s_wf + nrw;
+    uint8_t* s_map2 = s_lv + 64;
     for (uint32_t i = threadIdx.x; i < a.ny; i += 256) s_yt[i] = a.yt[i];
     if (threadIdx.x < a.nt) s_lv[threadIdx.x] = a.lv[threadIdx.x];
+    if (threadIdx.x < 64u) s_map2[threadIdx.x] = threadIdx.x < a.n2 ? a.map2[threadIdx.x] : (uint8_t)0xffu;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nrw; i += 256) s_wf[i] = a.wflags[s_yt[i >> 4].tile * 16u + (i & 15u)];
     for (uint32_t i = lane; i < accw; i += 64) s_acc[i] = 0ull;
@@ -258,8 +267,14 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
             };
             const int32_t np0 = min(64, end - beg);
             t_col += (uint32_t)max(0, end - beg);
+            if (a.own) t_sl += a.n2 ? 4u : 2u;  // the own slots' lines
             unsigned long long ovf = 0ull;
             issue(cid_cur, 0);
+            // own slots (lanes 0-15: F_{t-1}'s two lines, 16-31: F_{t-2}'s), with the first batch
+            ulonglong2 qo = make_ulonglong2(~0ull, ~0ull);
+            if (a.own && (lane < 16u || (lane < 32u && a.n2)))
+                qo = *reinterpret_cast<const ulonglong2*>((lane < 16u ? a.slot_cur : a.slot_next) + v * kSlotU16 +
+                                                          (lane & 15u) * 8u);
             uint32_t h_next = 0u;
             const uint32_t cid_next = load_ids(jn + 1u, h_next);  // the next node's peers
             consume(cid_cur, 0, np0, ovf);
@@ -282,6 +297,39 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                 }
                 fallback(cid, ovf2);
             }
+            // ---- own-frontier dedup: clear the incoming bits the node already holds ----
+            // The floods are breadth-first searches advancing one hop per tick, so a node v adjacent
+            // to a peer u that first saw share s at tick t-1 first saw s at t-2, t-1 or t (v's
+            // sends reach u one tick later, and u's reach v).  So among v's incoming bits at tick t
+            // the processed ones (p2pnode.cc:189) are exactly v's frontier bits of ticks t-1 and
+            // t-2: v's own slots, already in registers -- no dependent load of v's seen words.  Id
+            // group words (several sources for one id, group_fix) and nodes whose own slot
+            // overflowed (their frontier is in dense rows) still read seen (need_sv below).
+            bool own_ovf = !a.own;
+            if (a.own) {
+                const uint32_t h1 = (uint32_t)__shfl((int)(qo.x & 0xffffull), 0, 64);
+                const uint32_t h2 = (uint32_t)__shfl((int)(qo.x & 0xffffull), 16, 64);
+                own_ovf = h1 == kSlotOverflow || (a.n2 && h2 == kSlotOverflow);
+                if (!own_ovf) {
+                    __builtin_amdgcn_wave_barrier();
+                    const uint32_t piece = lane & 15u;  // 16-B piece: 0-7 first line, 8-15 second
+                    const bool prev2 = lane >= 16u;
+                    const bool valid = lane < 32u && (!prev2 || a.n2) && (piece < 8u || (prev2 ? h2 : h1) > 63u);
+                    if (valid) {
+#pragma unroll
+                        for (int j = 0; j < 8; j++) {
+                            const uint32_t e = (j == 0 && piece == 0u) ? kSlotTomb : slot_entry(qo, j);
+                            if (e == kSlotTomb) continue;
+                            uint32_t w = e >> 6;  // F_{t-1}: read position r * 16 + word
+                            if (prev2) {          // F_{t-2}: t-2's write index -> read position
+                                const uint32_t r = s_map2[e >> 10];
+                                w = r == 0xffu ? spare : r * 16u + ((e >> 6) & 15u);
+                            }
+                            atomicAnd(&s_acc[min(w, spare)], ~(1ull << (e & 63u)));
+                        }
+                    }
+                }
+            }
             __builtin_amdgcn_wave_barrier();
             // ---- touched words -> list ----
             uint32_t ntouch = 0;
@@ -294,6 +342,7 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
             }
             __builtin_amdgcn_wave_barrier();
             // ---- dedup against the own seen words (the first 4 x 64 loads issued together) ----
+            // (own-frontier dedup: only for id-group words, or every word of an overflowed node)
             uint32_t cnt = 0, cnt_sp = 0;
             uint64_t svq[4];
 #pragma unroll
@@ -302,7 +351,8 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                 svq[r] = 0ull;
                 if (t < ntouch) {
                     const uint32_t i = s_list[t];
-                    svq[r] = a.seen[v * stride + s_yt[i >> 4].tile * 16u + (i & 15u)];
+                    if (own_ovf || (s_wf[i] & WF_GROUP))
+                        svq[r] = a.seen[v * stride + s_yt[i >> 4].tile * 16u + (i & 15u)];
                 }
             }
             for (uint32_t t0 = 0; t0 < ntouch; t0 += 64) {
@@ -312,21 +362,28 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                 const YoungTile yt = s_yt[i >> 4];
                 const uint32_t w = yt.tile * 16u + (i & 15u);
                 uint64_t x = 0ull;
+                bool need_sv = false;
                 if (valid) {
                     const uint32_t f = s_wf[i];
+                    need_sv = own_ovf || (f & WF_GROUP);
                     uint64_t* sp = a.seen + v * stride + w;
                     const uint32_t r = t0 >> 6;
-                    const uint64_t sv = r == 0 ? svq[0] : r == 1 ? svq[1] : r == 2 ? svq[2] : r == 3 ? svq[3] : *sp;
+                    const uint64_t sv = !need_sv ? 0ull : r == 0 ? svq[0] : r == 1 ? svq[1] : r == 2 ? svq[2] : r == 3 ? svq[3] : *sp;
                     const uint64_t keep = (f & WF_KEEP) ? a.ctl[w].keep : ~0ull;
                     x = s_acc[i] & ~sv & keep;
                     if (f & WF_GROUP) x = group_fix(x, sv, a.ctl[w].gmask, a.ctl[w].gstart);
-                    if (x) *sp = sv | x;
+                    if (x) {
+                        if (need_sv)
+                            *sp = sv | x;
+                        else  // (no-return atomic: the word's old value is not needed)
+                            atomicOr(reinterpret_cast<unsigned long long*>(sp), (unsigned long long)x);
+                    }
                     if (a.snap && (f & WF_SNAP)) snap_local += (unsigned long long)__popcll(x & a.ctl[w].snap);
                     s_acc[i] = x;  // the node's new bits, for the outputs below
                 }
                 cnt += (uint32_t)__popcll(x);
                 if (yt.flags & YT_WRITE) cnt_sp += (uint32_t)__popcll(x);
-                t_srd += wave_count(valid);
+                t_srd += wave_count(need_sv);
                 t_swr += wave_count(x != 0ull);
             }
             __builtin_amdgcn_wave_barrier();

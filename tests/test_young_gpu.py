@@ -64,6 +64,19 @@ def test_young_sparse_4096(gossip, oracle, cap, age):
         assert c.young_fallback_rows > 0  # overflowed peers were read through dense rows
 
 
+@pytest.mark.parametrize("cap,id_mask", [(3, 0), (127, 0), (127, 0x3FF)])
+def test_young_own_frontier_dedup(gossip, oracle, cap, id_mask):
+    # young_own 1: incoming bits deduped against the node's own frontier of the last two ticks
+    # (its own slots); seen is read only for id-group words and overflowed nodes
+    c = _parity(gossip, oracle, 3000, 12.0 / 2999, 81, 6.0, 5.0,
+                dict(young_cap=cap, young_age=4, young_own=1), id_mask=id_mask, flags=gossip.F_TILE_PER_TICK)
+    assert c.young_seen_writes > 0
+    if not id_mask and c.young_fallback_rows == 0:  # no id group, no overflowed slot: no seen read
+        assert c.young_seen_reads == 0
+    if cap == 3:
+        assert c.young_fallback_rows > 0 and c.young_seen_reads > 0  # overflowed nodes read seen
+
+
 @pytest.mark.parametrize("cap", [2, 127])
 def test_young_collisions(gossip, oracle, cap):
     # 0x3FF id mask: id groups of several sources; group births resolve against slot arrivals
