@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void k_transpose(const uint64_t* __restrict__ 
                                                    const unsigned long long* __restrict__ nz,
                                                    uint32_t ntw, uint32_t* __restrict__ FT) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t chunk = blockIdx.x * 4u + (threadIdx.x >> 6);  // 64-node chunk
+    const uint32_t chunk = blockIdx.x * 4u + wave_in_block();  // 64-node chunk
     const uint32_t w = blockIdx.y;
     if (w >= nwords || chunk * 64u >= kw * 32u) return;
     if (live_prev) {  // a 4-word column tile with no live word is skipped by the GEMM
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(1024) void k_dense_dedup(PullArgs a) {
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t stride = a.stride;
-    const uint64_t wave = (uint64_t)blockIdx.x * kDedupWaves + (threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * kDedupWaves + wave_in_block();
     const uint64_t nwaves = (uint64_t)gridDim.x * kDedupWaves;
     const uint32_t npass = (a.wact + 127u) / 128u;
     unsigned long long snap_local = 0ull;

@@ -148,6 +148,14 @@ __device__ __forceinline__ void acct_add(unsigned long long* acct, uint32_t slot
     atomicAdd(&acct[(blockIdx.x & (kAcctReplicas - 1u)) * kAcctSlots + slot], v);
 }
 
+// The index of the calling wave in its block, as a wave-uniform (scalar) value: the compiler's
+// uniformity analysis treats threadIdx.x >> 6 as divergent, which put every per-wave node index
+// and row address derived from it in VGPR pairs (64-bit VALU arithmetic, registers held across
+// the kernels' node loops).
+__device__ __forceinline__ uint32_t wave_in_block() {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
+
 #include "pull_kernel.h"
 #include "dense_kernel.h"
 #include "young_kernel.h"
@@ -2034,7 +2042,7 @@ __global__ __launch_bounds__(256) void k_move_rows(uint64_t* __restrict__ F, uin
                                                    uint64_t r0 = 0, uint64_t r1 = ~0ull,
                                                    const uint64_t* __restrict__ total = nullptr) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * 4u + wave_in_block();
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     if (total) r1 = min(r1, *total);
     for (uint64_t i = wave; i < k; i += nwaves) {

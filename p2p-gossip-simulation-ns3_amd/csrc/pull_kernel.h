@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     const uint32_t gl = lane % GRP, wl = gl % LPW, el = gl / LPW, slot = lane / GRP;
     const uint64_t stride = a.stride;
     const uint64_t n = a.n;
-    const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * 4u + wave_in_block();
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     // Pass geometry: consecutive 2 LPW-word passes, or (pull_tiles) LPW / 8 listed tiles per pass
     constexpr uint32_t TPP = LPW >= 8 ? (uint32_t)LPW / 8u : 1u;
@@ -559,7 +559,7 @@ __global__ __launch_bounds__(256) void k_pull_wide(PullArgs a) {
     const uint32_t tl = lane >> 3;  // tile of this lane inside a pass
     const uint64_t stride = a.stride;
     const uint64_t n = a.n;
-    const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * 4u + wave_in_block();
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint32_t npass = (a.wact + 127u) / 128u;
     const char* Fbytes = reinterpret_cast<const char*>(a.Fcur);

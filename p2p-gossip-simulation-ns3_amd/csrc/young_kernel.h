@@ -105,11 +105,30 @@ __host__ __device__ constexpr size_t young_lds_bytes(uint32_t ny, uint32_t nr) {
            (size_t)ny * sizeof(YoungTile) + (size_t)nr * 16u + 64u + 64u;
 }
 
+// Lane `src` of v (ds_bpermute), its address computed from the caller's `lane`: HIP's __shfl
+// derives the address from its own lane-id read, which the compiler hoists out of the kernels'
+// loops, one live register per distinct source expression.
+__device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+// v of lane `src`, src wave-uniform (v_readlane: no LDS trip; reads inactive lanes too)
+__device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)src);
+}
+// Sum over the wave (every lane active), wave-uniform: DPP inside each row of 16, then 4 reads.
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // lane ^ 1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);   // lane ^ 2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);  // other quad of 8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);  // other 8 of 16
+    return lane_read(x, 0) + lane_read(x, 16) + lane_read(x, 32) + lane_read(x, 48);
+}
+
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane) {
     uint32_t s = x;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)s, off, 64);
+        const uint32_t y = lane_get(s, lane - (uint32_t)off);
         if (lane >= (uint32_t)off) s += y;
     }
     return s - x;
@@ -119,6 +138,14 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane) {
 __device__ __forceinline__ uint32_t slot_entry(const ulonglong2& q, int j) {
     const uint64_t word = j < 4 ? q.x : q.y;
     return (uint32_t)(word >> (16 * (j & 3))) & 0xffffu;
+}
+
+// x, recomputed where it is used: an empty asm that "modifies" x keeps the compiler from hoisting
+// lane-derived values (slot offsets, shuffle addresses, spare words) out of the node loop, where
+// ~30 of them stayed live across the whole loop and set the kernel's register count
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
 }
 
 __device__ __forceinline__ uint32_t lanes_below(unsigned long long m, uint32_t lane) {
@@ -131,7 +158,7 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
     extern __shared__ unsigned long long smem[];
     const uint32_t nrw = a.nr * 16u;  // accumulated words
     const uint32_t accw = nrw + kYoungSpare;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t lane_id = threadIdx.x & 63u, wv = wave_in_block();
     unsigned long long* s_acc = smem + wv * accw;
     uint16_t* s_list = reinterpret_cast<uint16_t*>(smem + 4u * accw) + wv * nrw;
     uint16_t* s_out = reinterpret_cast<uint16_t*>(smem + 4u * accw) + 4u * nrw + wv * kSlotU16;  // 16-B aligned
@@ -144,7 +171,7 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
     if (threadIdx.x < 64u) s_map2[threadIdx.x] = threadIdx.x < a.n2 ? a.map2[threadIdx.x] : (uint8_t)0xffu;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nrw; i += 256) s_wf[i] = a.wflags[s_yt[i >> 4].tile * 16u + (i & 15u)];
-    for (uint32_t i = lane; i < accw; i += 64) s_acc[i] = 0ull;
+    for (uint32_t i = lane_id; i < accw; i += 64) s_acc[i] = 0ull;
     if (blockIdx.x == 0)  // young tiles are alive by definition (see above)
         for (uint32_t i = threadIdx.x; i < a.ny * 16u; i += 256)
             if (s_yt[i >> 4].flags) a.live[s_yt[i >> 4].tile * 16u + (i & 15u)] = ~0ull;
@@ -156,18 +183,8 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
     // traffic (wave-uniform): slot lines, peer ids, dense fallback rows, seen r/w, row/slot writes
     uint32_t t_sl = 0, t_col = 0, t_fb = 0, t_srd = 0, t_swr = 0, t_rw = 0, t_slw = 0, t_miss = 0;
 
-    // the 8 entries of a lane's 16-B piece of a slot line; `hdr`: entry 0 is the line's header
-    const uint32_t spare = nrw + (lane & (kYoungSpare - 1u));
-    auto scatter8 = [&](const ulonglong2& q, bool hdr) {
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint32_t e = (j == 0 && hdr) ? kSlotTomb : slot_entry(q, j);
-            // (w >= nrw lands in [nrw, spare] -- the spare words)
-            atomicOr(&s_acc[min(e >> 6, spare)], 1ull << (e & 63u));
-        }
-    };
-
     for (uint64_t c0 = a.v0 + wave * 64u; c0 < a.n; c0 += nwaves * 64u) {
+        const uint32_t lane = opaque(lane_id);
         const uint32_t cnt_nodes = (uint32_t)min<uint64_t>(64u, a.n - c0);
         const int64_t rp = a.rowptr[c0 + min(lane, cnt_nodes)];
         const int64_t rp_end = a.rowptr[c0 + cnt_nodes];
@@ -175,8 +192,8 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
         // (the peer's id and its hint byte, combined only when the node's gather starts: bit 31
         // of the id says the peer's slot has a second line -- ids are < 2^31)
         auto load_ids = [&](uint32_t j, uint32_t& hint) -> uint32_t {
-            const int32_t b = __shfl((int)rp, (int)(j & 63u), 64);
-            const int32_t nx = __shfl((int)rp, (int)((j + 1u) & 63u), 64);
+            const int32_t b = (int32_t)lane_read((uint32_t)rp, j & 63u);
+            const int32_t nx = (int32_t)lane_read((uint32_t)rp, (j + 1u) & 63u);
             const int32_t e = j + 1u < 64u ? nx : (int32_t)rp_end;
             hint = 0u;
             if (!(j < cnt_nodes && (int32_t)lane < e - b)) return 0xffffffffu;
@@ -190,9 +207,21 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
         uint32_t cid_cur = load_ids(0u, h_cur);
         cid_cur = with_hint(cid_cur, h_cur);
         for (uint32_t jn = 0; jn < cnt_nodes; jn++) {
+            const uint32_t lane = opaque(lane_id);
             const uint64_t v = c0 + jn;
-            const int32_t beg = __shfl((int)rp, (int)jn, 64);
-            const int32_t nx = __shfl((int)rp, (int)((jn + 1u) & 63u), 64);
+            // the 8 entries of a lane's 16-B piece of a slot line; `hdr`: entry 0 is the line's header
+            const uint32_t spare = nrw + (lane & (kYoungSpare - 1u));
+            auto scatter8 = [&](const ulonglong2& q, bool hdr) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const uint32_t e = (j == 0 && hdr) ? kSlotTomb : slot_entry(q, j);
+                    // (w >= nrw lands in [nrw, spare] -- the spare words).  32-bit LDS atomics on
+                    // the half word holding the bit: half the data moved per lane, one mask register
+                    atomicOr(reinterpret_cast<uint32_t*>(s_acc + min(e >> 6, spare)) + ((e >> 5) & 1u), 1u << (e & 31u));
+                }
+            };
+            const int32_t beg = (int32_t)lane_read((uint32_t)rp, jn);
+            const int32_t nx = (int32_t)lane_read((uint32_t)rp, (jn + 1u) & 63u);
             const int32_t end = jn + 1u < 64u ? nx : (int32_t)rp_end;
             // ---- gather: peers' slots -> accumulator, in batches of 8 kYoungQ peers ----
             // (the first batch is straight-line code: its loads go out before the next node's id
@@ -202,7 +231,7 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
 #pragma unroll
                 for (int k = 0; k < kYoungQ; k++) {
                     const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
-                    const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64);
+                    const uint32_t u = lane_get(cid, p);
                     q[k] = make_ulonglong2(~0ull, ~0ull);  // tombstones: nothing to scatter
                     q2[k] = make_ulonglong2(~0ull, ~0ull);
                     if (p < 64u && u != 0xffffffffu) {
@@ -219,10 +248,10 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                 for (int k = 0; k < kYoungQ; k++) {
                     if (pb + k * 8 >= np) break;  // (uniform) no peer in this group of 8
                     const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
-                    const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64);
+                    const uint32_t u = lane_get(cid, p);
                     const bool valid = p < 64u && u != 0xffffffffu;
                     const bool hinted = valid && (u & 0x80000000u);
-                    const uint32_t hdr = valid ? (uint32_t)__shfl((int)(q[k].x & 0xffffull), (int)(lane & ~7u), 64) : 0u;
+                    const uint32_t hdr = valid ? lane_get((uint32_t)(q[k].x & 0xffffull), lane & ~7u) : 0u;
                     t_sl += wave_count(valid && (lane & 7u) == 0u) + wave_count(hinted && (lane & 7u) == 0u);
                     // an overflowed slot's entries are a subset of its dense rows (read below)
                     scatter8(q[k], (lane & 7u) == 0u);
@@ -244,7 +273,7 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                         const bool miss = (missk >> k) & 1u;
                         if (!__ballot(miss)) continue;
                         const uint32_t p = (uint32_t)pb + (uint32_t)k * 8u + (lane >> 3);
-                        const uint32_t u = (uint32_t)__shfl((int)cid, (int)(p & 63u), 64) & 0x7fffffffu;
+                        const uint32_t u = lane_get(cid, p) & 0x7fffffffu;
                         ulonglong2 x = make_ulonglong2(~0ull, ~0ull);
                         if (miss) x = *reinterpret_cast<const ulonglong2*>(a.slot_cur + (uint64_t)u * kSlotU16 + 64u + (lane & 7u) * 8u);
                         t_miss += wave_count(miss && (lane & 7u) == 0u);
@@ -256,7 +285,7 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                 while (ovf) {  // overflowed peers: their dense rows of every read-sparse tile
                     const int p = __builtin_ctzll(ovf);
                     ovf &= ovf - 1ull;
-                    const uint32_t u = (uint32_t)__shfl((int)cid, p, 64) & 0x7fffffffu;
+                    const uint32_t u = lane_read(cid, (uint32_t)p) & 0x7fffffffu;
                     for (uint32_t i = lane; i < nrw; i += 64) {
                         if (!s_yt[i >> 4].flags) continue;  // a position whose tile is gone
                         const uint64_t x = a.Fcur[(uint64_t)u * stride + s_yt[i >> 4].tile * 16u + (i & 15u)];
@@ -307,8 +336,8 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
             // overflowed (their frontier is in dense rows) still read seen (need_sv below).
             bool own_ovf = !a.own;
             if (a.own) {
-                const uint32_t h1 = (uint32_t)__shfl((int)(qo.x & 0xffffull), 0, 64);
-                const uint32_t h2 = (uint32_t)__shfl((int)(qo.x & 0xffffull), 16, 64);
+                const uint32_t h1 = lane_read((uint32_t)(qo.x & 0xffffull), 0u);
+                const uint32_t h2 = lane_read((uint32_t)(qo.x & 0xffffull), 16u);
                 own_ovf = h1 == kSlotOverflow || (a.n2 && h2 == kSlotOverflow);
                 if (!own_ovf) {
                     __builtin_amdgcn_wave_barrier();
@@ -325,7 +354,7 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                                 const uint32_t r = s_map2[e >> 10];
                                 w = r == 0xffu ? spare : r * 16u + ((e >> 6) & 15u);
                             }
-                            atomicAnd(&s_acc[min(w, spare)], ~(1ull << (e & 63u)));
+                            atomicAnd(reinterpret_cast<uint32_t*>(s_acc + min(w, spare)) + ((e >> 5) & 1u), ~(1u << (e & 31u)));
                         }
                     }
                 }
@@ -389,7 +418,7 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
             __builtin_amdgcn_wave_barrier();
             cid_cur = with_hint(cid_next, h_next);  // (arrived long ago: the wait is before the stores)
             // ---- output: slot entries, or dense rows (overflowed / leaving the young set) ----
-            const uint32_t total = (uint32_t)wave_sum((unsigned long long)cnt_sp);
+            const uint32_t total = wave_sum32(cnt_sp);
             const bool overflow = total > a.cap;
             uint16_t* out = a.slot_next + v * kSlotU16;
             // the slot is staged in LDS and written as whole lines (no partial-line writes); every
@@ -410,7 +439,7 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                         x &= x - 1ull;
                         s_out[pos++] = (uint16_t)(((uint32_t)yt.w_idx << 10) | ((i & 15u) << 6) | bb);
                     }
-                    base += (uint32_t)wave_sum((unsigned long long)c);
+                    base += wave_sum32(c);
                 }
             }
             if (lane == 0) s_out[0] = (uint16_t)(overflow ? kSlotOverflow : total);
@@ -465,7 +494,7 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                 const uint32_t q = q0 + (lane >> 4);
                 if (q < a.ny) a.seen[v * stride + s_yt[q].tile * 16u + (lane & 15u)] = 0ull;
             }
-            const uint32_t c = (uint32_t)wave_sum((unsigned long long)cnt);
+            const uint32_t c = wave_sum32(cnt);
             if (lane == 0 && c) {  // no-return atomics: nothing waits on them
                 atomicAdd(&a.recv[v], c);
                 atomicAdd(reinterpret_cast<unsigned long long*>(&a.sent[v]), (unsigned long long)c * a.deg[v]);
@@ -474,9 +503,9 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
     }
     if (a.snap) {
         snap_local = wave_sum(snap_local);
-        if (lane == 0 && snap_local) atomicAdd(a.snap, snap_local);
+        if (lane_id == 0 && snap_local) atomicAdd(a.snap, snap_local);
     }
-    if (a.acct && lane == 0) {
+    if (a.acct && lane_id == 0) {
         const uint32_t tv[8] = {t_sl, t_col, t_fb, t_srd, t_swr, t_rw, t_slw, t_miss};
 #pragma unroll
         for (int q = 0; q < 8; q++)
