@@ -156,6 +156,34 @@ __device__ __forceinline__ uint32_t wave_in_block() {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 }
 
+// x, recomputed where it is used: an empty asm that "modifies" x keeps the compiler from hoisting
+// lane-derived values (slot offsets, shuffle addresses, spare words) out of the kernels' item loops,
+// where dozens of them stayed live across the whole loop and set the register counts (k_pull_young
+// 125 -> 64 VGPRs)
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+// Lane `src` of v (ds_bpermute), its address computed from the caller's `lane`: HIP's __shfl
+// derives the address from its own lane-id read, which the compiler hoists out of the kernels'
+// loops, one live register per distinct source expression.
+__device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+// v of lane `src`, src wave-uniform (v_readlane: no LDS trip; reads inactive lanes too)
+__device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)src);
+}
+// Sum over the wave (every lane active), wave-uniform: DPP inside each row of 16, then 4 reads.
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // lane ^ 1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);   // lane ^ 2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);  // other quad of 8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);  // other 8 of 16
+    return lane_read(x, 0) + lane_read(x, 16) + lane_read(x, 32) + lane_read(x, 48);
+}
+
 #include "pull_kernel.h"
 #include "dense_kernel.h"
 #include "young_kernel.h"

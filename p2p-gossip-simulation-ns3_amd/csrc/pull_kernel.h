@@ -56,19 +56,31 @@ __device__ __forceinline__ uint32_t dpp_or_step(uint32_t x) {
     return x | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
 }
 template <int G>
-__device__ __forceinline__ uint32_t group_or(uint32_t x) {
+__device__ __forceinline__ uint32_t group_or(uint32_t x, uint32_t lane = 0u) {  // lane: for G >= 32
     static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "group size");
     if constexpr (G >= 2) x = dpp_or_step<0xB1>(x);   // quad_perm [1,0,3,2]: lane ^ 1
     if constexpr (G >= 4) x = dpp_or_step<0x4E>(x);   // quad_perm [2,3,0,1]: lane ^ 2
     if constexpr (G >= 8) x = dpp_or_step<0x141>(x);  // row_half_mirror: the other quad of the 8
     if constexpr (G >= 16) x = dpp_or_step<0x140>(x); // row_mirror: the other 8 of the row
-    if constexpr (G >= 32) x |= (uint32_t)__shfl_xor((int)x, 16, 64);
-    if constexpr (G >= 64) x |= (uint32_t)__shfl_xor((int)x, 32, 64);
+    if constexpr (G >= 32) x |= lane_get(x, lane ^ 16u);
+    if constexpr (G >= 64) x |= lane_get(x, lane ^ 32u);
     return x;
 }
 template <int G>
-__device__ __forceinline__ unsigned long long group_or64(unsigned long long x) {
-    return (unsigned long long)group_or<G>((uint32_t)x) | ((unsigned long long)group_or<G>((uint32_t)(x >> 32)) << 32);
+__device__ __forceinline__ unsigned long long group_or64(unsigned long long x, uint32_t lane) {
+    return (unsigned long long)group_or<G>((uint32_t)x, lane) |
+           ((unsigned long long)group_or<G>((uint32_t)(x >> 32), lane) << 32);
+}
+// Sum over aligned groups of G lanes (every lane of a group active), DPP up to 16 lanes.
+template <int G>
+__device__ __forceinline__ uint32_t group_add(uint32_t x, uint32_t lane) {
+    if constexpr (G >= 2) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);
+    if constexpr (G >= 4) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);
+    if constexpr (G >= 8) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);
+    if constexpr (G >= 16) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);
+    if constexpr (G >= 32) x += lane_get(x, lane ^ 16u);
+    if constexpr (G >= 64) x += lane_get(x, lane ^ 32u);
+    return x;
 }
 
 // WF_YOUNG: the word belongs to a young tile, which k_pull_young owns this tick (young_kernel.h)
@@ -77,7 +89,10 @@ enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u, WF_Y
 
 constexpr uint32_t kPullLdsWords = 2048;  // words per launch: LDS liveness, new liveness, flags
 #ifndef PULL_INFLIGHT
-#define PULL_INFLIGHT 8  // A/B builds: make variants (q4, q12, q16)
+// 6 peer-row loads in flight per lane: k_pull<32,1> then holds 93 VGPRs, 5 waves per SIMD (8 in
+// flight: 100 VGPRs, 4 waves); C4 shard, same box: k_pull alone 53.0 -> 50.0 ms, the early exit
+// tested every 6 peers reads 5 % fewer rows (profiles/r03/ab/r3p2_*).  A/B builds: make variants
+#define PULL_INFLIGHT 6
 #endif
 constexpr int kInflight = PULL_INFLIGHT;  // peer-row loads in flight per lane
 // Non-temporal row accesses: a template switch of k_pull<LPW,1>, chosen at launch by bitmap size
@@ -119,8 +134,8 @@ __device__ __forceinline__ uint32_t pull_cid_load(const PullArgs& a, uint32_t st
                                                   uint32_t slot) {
     constexpr int NPW = 64 / (LPW * EPN);
     const uint32_t idx = step * NPW + slot;
-    const int32_t beg = __shfl((int)rp, (int)idx, 64);
-    const int32_t nx = __shfl((int)rp, (int)((idx + 1u) & 63u), 64);
+    const int32_t beg = (int32_t)lane_get((uint32_t)rp, idx);
+    const int32_t nx = (int32_t)lane_get((uint32_t)rp, (idx + 1u) & 63u);
     const int32_t end = (idx + 1u < 64u) ? nx : (int32_t)rp_end;
     const int32_t jj = beg + (int32_t)gl;
     return (c0 + idx < a.n && jj < end) ? (uint32_t)a.col[jj] : 0xffffffffu;
@@ -155,8 +170,12 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     }
     for (uint32_t i = threadIdx.x; i < a.nptile; i += 256) s_pt[i] = a.ptile[i];
     __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gl = lane % GRP, wl = gl % LPW, el = gl / LPW, slot = lane / GRP;
+    const uint32_t lane_id = threadIdx.x & 63u;
+    // lane geometry, recomputed inside the loops from an opaque lane id (engine.hip, opaque)
+#define PULL_LANES                                                                             \
+    const uint32_t lane = opaque(lane_id);                                                    \
+    const uint32_t gl = lane % GRP, wl = gl % LPW, el = gl / LPW, slot = lane / GRP;          \
+    (void)el;
     const uint64_t stride = a.stride;
     const uint64_t n = a.n;
     const uint64_t wave = (uint64_t)blockIdx.x * 4u + wave_in_block();
@@ -166,7 +185,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     const bool listed = a.ptile != nullptr;
     const uint32_t npass = listed ? a.nptile / TPP : (a.wact + 2u * LPW - 1u) / (2u * LPW);
     // launch-local word of this lane's pair in pass p (kNoWord: none)
-    auto lw_of = [&](uint32_t p) -> uint32_t {
+    auto lw_of = [&](uint32_t p, uint32_t wl) -> uint32_t {
         if (!listed) {
             const uint32_t x = p * 2u * LPW + 2u * wl;
             return x < a.wact ? x : kNoWord;
@@ -196,6 +215,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     const bool gather = a.inc == nullptr && EPN == 1;  // the pipelined id/occupancy loads
 
     for (uint64_t c0 = a.v0 + wave * 64u; npass && c0 < n; c0 += nwaves * 64u) {
+        PULL_LANES
         const int64_t rp = a.rowptr[min(c0 + lane, n)];
         const int64_t rp_end = a.rowptr[min(c0 + 64u, n)];
         // item k = (step, pass): node c0 + step * NPW + slot, the lane's word pair lw_of(pass)
@@ -203,7 +223,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
         ulonglong2 s2c = make_ulonglong2(0ull, 0ull);
         {
             const uint64_t v = c0 + slot;
-            const uint32_t lw = lw_of(0u);
+            const uint32_t lw = lw_of(0u, wl);
             if (v < n && lw != kNoWord && (s_lp[lw] | s_lp[lw + 1u]) != 0ull)
                 s2c = load_row16<NT>(a.seen + v * stride + a.wbase + lw);
         }
@@ -230,18 +250,19 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
         // pending first-item load would make every item wait for its own prefetches)
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
         while (step < nsteps) {
+            PULL_LANES
             // ---- geometry of this item and the next two ----
             const uint32_t step1 = pass + 1u < npass ? step : step + 1u;
             const uint32_t pass1 = pass + 1u < npass ? pass + 1u : 0u;
             const uint32_t step2 = pass1 + 1u < npass ? step1 : step1 + 1u;
             const uint32_t idx = step * NPW + slot;
             const uint32_t v = (uint32_t)(c0 + idx);
-            const uint32_t lw0 = lw_of(pass);
+            const uint32_t lw0 = lw_of(pass, wl);
             const uint32_t w = a.wbase + (lw0 == kNoWord ? 0u : lw0);
             const bool act = c0 + idx < n && lw0 != kNoWord;
             if (pass == 0u) {  // (uniform) a new node: its peer range, with the whole wave active
-                beg = __shfl((int)rp, (int)idx, 64);
-                const int32_t nxb = __shfl((int)rp, (int)((idx + 1u) & 63u), 64);
+                beg = (int32_t)lane_get((uint32_t)rp, idx);
+                const int32_t nxb = (int32_t)lane_get((uint32_t)rp, (idx + 1u) & 63u);
                 end = (idx + 1u < 64u) ? nxb : (int32_t)rp_end;
             }
             const uint32_t tw = tw_of(pass);  // (uniform: the pass's occupancy word)
@@ -250,14 +271,14 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             bool s2n_gated = false;
             if (gate && nz_new) {  // (uniform) this item starts a new occupancy word
                 unsigned long long x = nz0;
-                x = group_or64<GRP>(x);
+                x = group_or64<GRP>(x, lane);
                 nzor = x;
                 nz_new = false;
             }
             if (step1 < nsteps) {
                 // (a dead pair's seen words are never needed: only cleared, never merged)
                 const uint64_t v1 = c0 + step1 * NPW + slot;
-                const uint32_t lw1 = lw_of(pass1);
+                const uint32_t lw1 = lw_of(pass1, wl);
                 // this item's peer range was read with the whole wave active (a shuffle inside
                 // the branch below would read the row pointers of lanes whose own pair is dead --
                 // inactive lanes give no data -- so a node with more peers than one lane group
@@ -303,9 +324,13 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             uint64_t k0 = ~0ull, k1 = ~0ull;
             if (act && (f0 & WF_KEEP)) k0 = s_keep[w - a.wbase];
             if (act && (f1 & WF_KEEP)) k1 = s_keep[w + 1 - a.wbase];
+            // Bits that can still become new (direction-optimising BFS, bottom-up): every F_cur
+            // bit -- so every incoming bit -- lies inside live_prev, and seen / not-kept bits are
+            // masked out of `new`, so new = incoming & want (and peers beyond covering `want`
+            // add nothing).  Only `want` is carried past the gather.
+            const uint64_t want0 = lp0 & ~s2.x & k0, want1 = lp1 & ~s2.y & k1;
             // (incoming mode must consume every live pair's incoming word: no saturation skip)
-            const bool need = act && !dead && !s2c_gated &&
-                              (a.noskip || a.inc || ((lp0 & ~s2.x & k0) | (lp1 & ~s2.y & k1)) != 0ull);
+            const bool need = act && !dead && !s2c_gated && (a.noskip || a.inc || (want0 | want1) != 0ull);
             // Columns are allocated in 16-word tiles (one 128-B line per row, engine.hip), so the
             // read decision is made per tile: the 8 word-lanes of a tile load together and every
             // fetched line is fully used.
@@ -313,7 +338,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             tn = (int)group_or<8>((uint32_t)tn);  // per tile (8 word-lanes)
             const bool tneed = tn != 0 && act;
             int gneed = tn;
-            gneed = (int)group_or<GRP>((uint32_t)gneed);
+            gneed = (int)group_or<GRP>((uint32_t)gneed, lane);
             // ---- gather peer rows ----
             const unsigned long long tbit = 1ull << ((w >> 4) & 63u);
             uint64_t acc0 = 0ull, acc1 = 0ull;
@@ -330,10 +355,6 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             } else if (gneed) {  // uniform inside the node group
                 const uint64_t* Fw = a.Fcur + w;
                 if constexpr (EPN == 1) {
-                    // Bits that can still become new (direction-optimising BFS, bottom-up):
-                    // every F_cur bit lies inside live_prev, and seen / not-kept bits are
-                    // masked out of `new`, so peers beyond covering these add nothing.
-                    const uint64_t want0 = lp0 & ~s2.x & k0, want1 = lp1 & ~s2.y & k1;
                     // late tiles (WF_LATE, set by the host from the tile's age): dense frontier
                     // rows, few unseen bits -- stop at the first batch that covers them all
                     const bool late = ((f0 | f1) & WF_LATE) != 0u;
@@ -347,13 +368,14 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                                            ? 1 : (((want0 & ~acc0) | (want1 & ~acc1)) != 0ull);
                             open = (int)group_or<8>((uint32_t)open);  // per tile (8 word-lanes)
                             int gopen = open;
-                            gopen = (int)group_or<GRP>((uint32_t)gopen);
+                            gopen = (int)group_or<GRP>((uint32_t)gopen, lane);
                             if (!gopen) break;  // uniform inside the node group
                             uint32_t u[kInflight], z[kInflight];
 #pragma unroll
                             for (int t = 0; t < kInflight; t++) {
-                                u[t] = (uint32_t)__shfl((int)cid, (t0 + t) & (GRP - 1), GRP);
-                                z[t] = (uint32_t)__shfl((int)nzp, (t0 + t) & (GRP - 1), GRP);
+                                const uint32_t src = (lane & ~(uint32_t)(GRP - 1)) | ((uint32_t)(t0 + t) & (GRP - 1u));
+                                u[t] = lane_get(cid, src);
+                                z[t] = lane_get(nzp, src);
                             }
                             ulonglong2 q[kInflight];
 #pragma unroll
@@ -418,15 +440,16 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             if constexpr (EPN > 1) {
 #pragma unroll
                 for (int off = LPW; off < GRP; off <<= 1) {
-                    acc0 |= __shfl_xor(acc0, off, GRP);
-                    acc1 |= __shfl_xor(acc1, off, GRP);
+                    const uint32_t src = lane ^ (uint32_t)off;
+                    acc0 |= (uint64_t)lane_get((uint32_t)acc0, src) | ((uint64_t)lane_get((uint32_t)(acc0 >> 32), src) << 32);
+                    acc1 |= (uint64_t)lane_get((uint32_t)acc1, src) | ((uint64_t)lane_get((uint32_t)(acc1 >> 32), src) << 32);
                 }
             }
             // ---- dedup ----
             uint64_t n0 = 0ull, n1 = 0ull;
             if (act && el == 0 && !dead) {
-                n0 = acc0 & ~s2.x & k0;
-                n1 = acc1 & ~s2.y & k1;
+                n0 = acc0 & want0;
+                n1 = acc1 & want1;
                 if (f0 & WF_GROUP) n0 = group_fix(n0, s2.x, a.ctl[w].gmask, a.ctl[w].gstart);
                 if (f1 & WF_GROUP) n1 = group_fix(n1, s2.y, a.ctl[w + 1].gmask, a.ctl[w + 1].gstart);
             }
@@ -465,7 +488,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             // ---- occupancy word of this node, written whole once per nz word index ----
             {
                 unsigned long long nb = (ta && own && (wl & 7u) == 0u) ? tbit : 0ull;
-                nb = group_or64<GRP>(nb);
+                nb = group_or64<GRP>(nb, lane);
                 nzacc |= nb;
                 const bool last_of_tw = pass + 1u == npass || tw_of(pass + 1u) != tw;
                 if (last_of_tw) {
@@ -480,9 +503,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             }
             // ---- per-node counters after the node's last pass ----
             if (pass + 1u == npass) {
-                uint32_t c = cnt;
-#pragma unroll
-                for (int off = GRP / 2; off > 0; off >>= 1) c += __shfl_xor(c, off, GRP);
+                const uint32_t c = group_add<GRP>(cnt, lane);
                 if (gl == 0 && c) {
                     if (a.shared_out) {  // no-return atomics: nothing waits on them
                         atomicAdd(&a.recv[v], c);
@@ -507,9 +528,9 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     }
     if (a.snap) {
         snap_local = wave_sum(snap_local);
-        if (lane == 0 && snap_local) atomicAdd(a.snap, snap_local);
+        if (lane_id == 0 && snap_local) atomicAdd(a.snap, snap_local);
     }
-    if (a.acct && lane == 0) {
+    if (a.acct && lane_id == 0) {
         const uint32_t tv[6] = {t_pe, t_col, t_srd, t_swr, t_fwr, t_nz};
         const int slot_of[6] = {0, 1, 2, 3, 4, 7};
 #pragma unroll
@@ -521,6 +542,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
         const unsigned long long x = s_new[i];
         if (x) atomicOr(&a.live[a.wbase + i], x);
     }
+#undef PULL_LANES
 }
 
 // ------------------------------------------------------------------------------------------

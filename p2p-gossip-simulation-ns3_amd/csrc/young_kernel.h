@@ -105,25 +105,6 @@ __host__ __device__ constexpr size_t young_lds_bytes(uint32_t ny, uint32_t nr) {
            (size_t)ny * sizeof(YoungTile) + (size_t)nr * 16u + 64u + 64u;
 }
 
-// Lane `src` of v (ds_bpermute), its address computed from the caller's `lane`: HIP's __shfl
-// derives the address from its own lane-id read, which the compiler hoists out of the kernels'
-// loops, one live register per distinct source expression.
-__device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t src) {
-    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
-}
-// v of lane `src`, src wave-uniform (v_readlane: no LDS trip; reads inactive lanes too)
-__device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t src) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)src);
-}
-// Sum over the wave (every lane active), wave-uniform: DPP inside each row of 16, then 4 reads.
-__device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // lane ^ 1
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);   // lane ^ 2
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);  // other quad of 8
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);  // other 8 of 16
-    return lane_read(x, 0) + lane_read(x, 16) + lane_read(x, 32) + lane_read(x, 48);
-}
-
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane) {
     uint32_t s = x;
 #pragma unroll
@@ -138,14 +119,6 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane) {
 __device__ __forceinline__ uint32_t slot_entry(const ulonglong2& q, int j) {
     const uint64_t word = j < 4 ? q.x : q.y;
     return (uint32_t)(word >> (16 * (j & 3))) & 0xffffu;
-}
-
-// x, recomputed where it is used: an empty asm that "modifies" x keeps the compiler from hoisting
-// lane-derived values (slot offsets, shuffle addresses, spare words) out of the node loop, where
-// ~30 of them stayed live across the whole loop and set the kernel's register count
-__device__ __forceinline__ uint32_t opaque(uint32_t x) {
-    asm volatile("" : "+v"(x));
-    return x;
 }
 
 __device__ __forceinline__ uint32_t lanes_below(unsigned long long m, uint32_t lane) {
