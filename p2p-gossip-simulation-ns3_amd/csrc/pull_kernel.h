@@ -212,7 +212,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     unsigned long long snap_local = 0ull;
     uint32_t t_pe = 0, t_col = 0, t_srd = 0, t_swr = 0, t_fwr = 0, t_nz = 0;  // wave-uniform
     unsigned long long nzacc = 0ull;
-    const bool gather = a.inc == nullptr && EPN == 1;  // the pipelined id/occupancy loads
+    const bool gather = EPN == 1;  // the pipelined id/occupancy loads
 
     for (uint64_t c0 = a.v0 + wave * 64u; npass && c0 < n; c0 += nwaves * 64u) {
         PULL_LANES
@@ -329,8 +329,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             // masked out of `new`, so new = incoming & want (and peers beyond covering `want`
             // add nothing).  Only `want` is carried past the gather.
             const uint64_t want0 = lp0 & ~s2.x & k0, want1 = lp1 & ~s2.y & k1;
-            // (incoming mode must consume every live pair's incoming word: no saturation skip)
-            const bool need = act && !dead && !s2c_gated && (a.noskip || a.inc || (want0 | want1) != 0ull);
+            const bool need = act && !dead && !s2c_gated && (a.noskip || (want0 | want1) != 0ull);
             // Columns are allocated in 16-word tiles (one 128-B line per row, engine.hip), so the
             // read decision is made per tile: the 8 word-lanes of a tile load together and every
             // fetched line is fully used.
@@ -342,17 +341,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             // ---- gather peer rows ----
             const unsigned long long tbit = 1ull << ((w >> 4) & 63u);
             uint64_t acc0 = 0ull, acc1 = 0ull;
-            if (a.inc) {
-                // DENSE mode: the gather already happened as an MFMA contraction; take the
-                // incoming words and leave them zeroed for the next tick.
-                if (tneed && el == 0) {
-                    ulonglong2* ip = reinterpret_cast<ulonglong2*>(a.inc + (uint64_t)v * stride + w);
-                    const ulonglong2 x = *ip;
-                    acc0 = x.x;
-                    acc1 = x.y;
-                    if ((acc0 | acc1) != 0ull) *ip = make_ulonglong2(0ull, 0ull);
-                }
-            } else if (gneed) {  // uniform inside the node group
+            if (gneed) {  // uniform inside the node group
                 const uint64_t* Fw = a.Fcur + w;
                 if constexpr (EPN == 1) {
                     // late tiles (WF_LATE, set by the host from the tile's age): dense frontier
