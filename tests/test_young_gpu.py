@@ -54,8 +54,9 @@ def _parity(gossip, oracle, n, p, seed, sim_s, lat_ms, opts, id_mask=0, flags=0,
     return c
 
 
-@pytest.mark.parametrize("cap", [1, 3, 127])
-@pytest.mark.parametrize("age", [1, 3, 6])
+# (5 of the 9 cap x age pairs: overflow-heavy, mid and roomy slots at the short, mid and long
+# ages -- keeps the -m gpu suite inside its time budget)
+@pytest.mark.parametrize("cap,age", [(1, 3), (1, 6), (3, 3), (127, 1), (127, 6)])
 def test_young_sparse_4096(gossip, oracle, cap, age):
     c = _parity(gossip, oracle, 4096, 16.0 / 4095, 71, 6.0, 5.0,
                 dict(young_cap=cap, young_age=age), flags=gossip.F_TILE_PER_TICK)
