@@ -174,6 +174,37 @@ def test_wide_window_kernels_agree(gossip, oracle):
             assert np.array_equal(getattr(st, k), getattr(r, k)), (kern, k)
 
 
+def test_tile_list_options_agree(gossip, oracle):
+    # k_pull's pass -> tile lists (pull_tiles) and their age order (pull_tile_order) only change
+    # which lanes serve which tiles: a wide window of tiles of every age (a fresh tile per tick),
+    # id collisions in play, must give the oracle's counters and trace under every setting.
+    n = 3000
+    topo = gossip.Topology.gnp(n, 8.0 / (n - 1), 45, gossip.TOPO_SKIP)
+    t_cut = gossip.seconds_to_ns(6.3)
+    ev = gossip.make_schedule(n, 9, T0, t_cut, id_mask=0xFFF)
+    a, b = topo.links()
+    r = oracle.run_replay(n, L, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=True)
+    tn, ti, tt, th, tv = r.trace
+    ok = np.lexsort((ti, tn))
+    for opts in ({}, {"pull_tile_order": 0}, {"pull_tiles": 0}):
+        eng = gossip.Engine(n, L, T0, t_cut, flags=gossip.F_TILE_PER_TICK | gossip.F_TRACE | gossip.F_GENERIC_PULL)
+        for k, v in opts.items():
+            eng.set_option(k, v)
+        eng.set_topology(topo)
+        eng.set_schedule(ev)
+        eng.run()
+        eng.sync()
+        st, c = eng.stats(), eng.counters()
+        assert c.words_hw > 64 and (c.pull_tiles == 0 or opts.get("pull_tiles") != 0), opts
+        for k in STATS:
+            assert np.array_equal(getattr(st, k), getattr(r, k)), (opts, k)
+        node, sid, tick, hop, via = eng.trace()
+        ek = np.lexsort((sid, node))
+        assert np.array_equal(node[ek], tn[ok]) and np.array_equal(sid[ek], ti[ok]), opts
+        assert np.array_equal(tick[ek], tt[ok] // L) and np.array_equal(via[ek], tv[ok]), opts
+        eng.close()
+
+
 def test_window_growth_is_transparent(gossip, oracle):
     # Start with a one-tile window: the engine must widen its rows mid-run and stay exact.
     n = 3000
