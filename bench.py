@@ -179,7 +179,7 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
         acc["young_sl"] += c1.young_slot_lines
         acc["young_fb"] += c1.young_fallback_rows
         for k in ("young_col_ids", "young_seen_reads", "young_seen_writes", "young_rows_written",
-                  "young_slot_writes", "young_line2_misses"):
+                  "young_slot_writes", "young_line2_misses", "young_fresh_lines"):
             acc[k] = acc.get(k, 0) + getattr(c1, k)
         acc["phase_ms"] += c1.pull_phase_ms
         acc["words_hw"] = max(acc["words_hw"], c1.words_hw)
@@ -465,6 +465,7 @@ def main():
                     "dense_rows_written": 128 * acc["young_rows_written"] / yl,
                     "slot_lines_written": 128 * acc["young_slot_writes"] / yl,
                     "unhinted_second_lines_read": 128 * acc.get("young_line2_misses", 0) / yl,
+                    "fresh_tile_seen_lines_cleared": 128 * acc.get("young_fresh_lines", 0) / yl,
                 },
             }
             t_young, why_young = pmc_traffic(wl["name"] + "_young", out, variant)

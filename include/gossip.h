@@ -369,6 +369,8 @@ typedef struct gossip_counters {
     uint64_t young_line2_misses; /* second slot lines fetched without a hint (k_pull_young) */
     uint32_t pull_late_age;      /* late_age in effect for the last pull (0: no early exit) */
     uint32_t pull_tiles;         /* 1: the last tick's k_pull passes ran over tile lists (option pull_tiles) */
+    uint64_t young_fresh_lines;  /* seen lines of fresh tiles cleared by k_pull_young [128 B]; in
+                                    young_bytes_moved */
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 /* Option rehearse_rows = R: per row block r < R, summed since the last reset_timing -- pull time,

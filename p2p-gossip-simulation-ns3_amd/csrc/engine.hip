@@ -667,6 +667,7 @@ struct gossip_engine {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers_young;
     double young_ms_done = 0.0;
     uint64_t young_launches = 0;
+    uint64_t young_fresh_lines = 0;  // fresh tiles' seen lines k_pull_young cleared (128 B each)
     // ---- timing / counters
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers;
     std::vector<hipEvent_t> event_pool;
@@ -1832,6 +1833,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 timers_young.emplace_back(y0, y1);
             }
             young_launches++;
+            young_fresh_lines += (uint64_t)(ny - ny_read) * (uint64_t)(v1 - v0);
             return GOSSIP_OK;
         };
         // DENSE mode: dedup of the incoming words of rows [base.v0, base.n), one node per wave
@@ -3402,8 +3404,9 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     c->young_line2_misses = acct[15];
     c->pull_late_age = (uint32_t)e->late_age_now();
     c->pull_tiles = e->pt_used ? 1u : 0u;
-    c->young_bytes_moved = 128ull * (acct[8] + acct[10] + acct[13] + acct[14] + acct[15]) + 5ull * acct[9] +
+    c->young_bytes_moved = 128ull * (acct[8] + acct[10] + acct[13] + acct[14] + acct[15] + e->young_fresh_lines) + 5ull * acct[9] +
                            8ull * (acct[11] + acct[12]) + e->young_launches * (8ull * (e->n + 1) + 16ull * e->n);
+    c->young_fresh_lines = e->young_fresh_lines;
     uint64_t g = 0;
     const uint64_t done = (uint64_t)std::max<int64_t>(0, std::min(e->cur, e->tick_end) - e->tick0);
     if (!e->tick_lo.empty()) g = e->tick_lo[std::min<uint64_t>(done, e->tick_lo.size() - 1)];
@@ -3448,6 +3451,7 @@ int gossip_engine_reset_timing(gossip_engine* e) {
     e->timers_young.clear();
     e->young_ms_done = 0.0;
     e->young_launches = 0;
+    e->young_fresh_lines = 0;
     for (auto& p : e->timers_phase) {
         e->event_pool.push_back(p.first);
         e->event_pool.push_back(p.second);

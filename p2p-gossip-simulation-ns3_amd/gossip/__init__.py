@@ -109,6 +109,7 @@ class gossip_counters(C.Structure):
         ("exchange_bytes_sent", C.c_uint64), ("exchange_bytes_received", C.c_uint64),
         ("pull_phase_ms", C.c_double), ("young_line2_misses", C.c_uint64),
         ("pull_late_age", C.c_uint32), ("pull_tiles", C.c_uint32),
+        ("young_fresh_lines", C.c_uint64),
     ]
 
 
