@@ -56,7 +56,7 @@ __device__ __forceinline__ uint32_t dpp_or_step(uint32_t x) {
     return x | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
 }
 template <int G>
-__device__ __forceinline__ uint32_t group_or(uint32_t x, uint32_t lane = 0u) {  // lane: for G >= 32
+__device__ __forceinline__ uint32_t group_or(uint32_t x, uint32_t lane) {  // lane: the caller's (G >= 32)
     static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "group size");
     if constexpr (G >= 2) x = dpp_or_step<0xB1>(x);   // quad_perm [1,0,3,2]: lane ^ 1
     if constexpr (G >= 4) x = dpp_or_step<0x4E>(x);   // quad_perm [2,3,0,1]: lane ^ 2
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             // read decision is made per tile: the 8 word-lanes of a tile load together and every
             // fetched line is fully used.
             int tn = need ? 1 : 0;
-            tn = (int)group_or<8>((uint32_t)tn);  // per tile (8 word-lanes)
+            tn = (int)group_or<8>((uint32_t)tn, lane);  // per tile (8 word-lanes)
             const bool tneed = tn != 0 && act;
             int gneed = tn;
             gneed = (int)group_or<GRP>((uint32_t)gneed, lane);
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                         for (int t0 = 0; t0 < rem; t0 += kInflight) {
                             int open = (a.noskip || !late)
                                            ? 1 : (((want0 & ~acc0) | (want1 & ~acc1)) != 0ull);
-                            open = (int)group_or<8>((uint32_t)open);  // per tile (8 word-lanes)
+                            open = (int)group_or<8>((uint32_t)open, lane);  // per tile (8 word-lanes)
                             int gopen = open;
                             gopen = (int)group_or<GRP>((uint32_t)gopen, lane);
                             if (!gopen) break;  // uniform inside the node group
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             // (NOSKIP diagnostic: every tile row is written and marked occupied, so the pull
             // reads every peer row -- the dense-pull byte count)
             int ta = (n0 | n1) != 0ull || (a.noskip && act);
-            ta = (int)group_or<8>((uint32_t)ta);
+            ta = (int)group_or<8>((uint32_t)ta, lane);
             // ---- state, counters (one lane per word pair) ----
             const bool own = act && el == 0;
             const bool swr = own && (dead ? ((f0 | f1) & WF_CLEAR) != 0u
