@@ -21,14 +21,17 @@
 // fresh write-sparse tiles; the tiles leaving the young set (read-sparse, write-dense) are written
 // back as dense rows with their occupancy bits, for k_pull to read next tick.
 //
-// Per node (one wave, ~4 dependent round trips: peer ids, slot lines, second lines, own seen
-// words): gather the peers' slots (8 lanes x 16 B per peer, 24 peers per batch) and scatter their
-// entries into a per-wave LDS accumulator of the read-sparse words; compact the touched words
-// into a list; dedup them against the own seen words (the same WordCtl masks as k_pull: keep, id
-// groups, snapshot), counters, the output slot (wave prefix sum of the entry counts) and the
-// dense rows of the tiles leaving the young set.  The code keeps few registers and ~5 KiB of LDS
-// per wave so that 7-8 waves per SIMD hide the round trips (an explicitly pipelined variant
-// measured no faster: the loop-carried registers forced vmcnt(0) waits, profiles/r02/).
+// Per node (one wave; dependent round trips: slot lines -- peer ids are prefetched a node ahead,
+// hinted second lines come with the first -- then the own seen words): gather the peers' slots
+// (8 lanes x 16 B per peer, 24 peers per batch) and scatter their entries into a per-wave LDS
+// accumulator of the read-sparse words; compact the touched words into a list; dedup them against
+// the own seen words (the same WordCtl masks as k_pull: keep, id groups, snapshot), counters, the
+// output slot (wave prefix sum of the entry counts) and the dense rows of the tiles leaving the
+// young set.  64 VGPRs (round 3: lane values recomputed per node, explicit-lane shuffles) and ~5
+// KiB of LDS per wave, so that 6-8 waves per SIMD hide the round trips (an explicitly pipelined
+// variant measured no faster: the loop-carried registers forced vmcnt(0) waits, profiles/r02/).
+// Option young_own replaces the seen-word dedup by the node's own frontier of ticks t-1 and t-2
+// (below); measured slower, off by default.
 // Fresh tiles' seen words are cleared here (row by row), and the young words'
 // liveness is reported as all-ones (a young tile is alive by definition; it retires after it
 // leaves the young set, through k_pull's exact liveness).
