@@ -278,6 +278,8 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *   "young_grid"       k_pull_young blocks, 0 = the pull grid                [GOSSIP_YOUNG_GRID]
  *   "young_waves"      k_pull_young register budget in waves per SIMD: 4 (no spills), 5, 6
  *                                                                         [GOSSIP_YOUNG_WAVES]
+ *   "young_nt"         1: k_pull_young reads its peers' slot lines non-temporally (default), 0:
+ *                      cached                                                  [GOSSIP_YOUNG_NT]
  *   "young_own"        1: k_pull_young dedups a node's incoming bits against its own frontier
  *                      of the last two ticks (its own slots, read with the peers'), reading
  *                      seen only for id-group words and overflowed nodes; 0: against its seen

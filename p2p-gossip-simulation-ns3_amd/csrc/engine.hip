@@ -643,6 +643,7 @@ struct gossip_engine {
     bool pt_used = false;                  // the last tick's k_pull ran over tile lists
     int64_t opt_young_waves = 4;      // k_pull_young register budget: waves per SIMD (4, 5, 6)
     int64_t opt_young_own = 0;        // k_pull_young dedups against the node's own last two frontiers
+    int64_t opt_young_nt = 1;         // k_pull_young reads peers' slot lines non-temporally
     int64_t opt_late_age = -1;        // k_pull early exit for tiles >= this many ticks old (0: off, -1: auto)
     int64_t late_age_now() const {    // auto: every tile of a gathering (CSR) pull
         return opt_late_age >= 0 ? opt_late_age : dense ? 0 : kAutoLateAge;
@@ -1811,6 +1812,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             y.map2 = d_young[slot]->map2;
             y.own = (opt_young_own && ny_read) ? 1u : 0u;
             y.n2 = y.own ? (uint32_t)std::min<size_t>(wt_last2.size(), 64) : 0u;
+            y.slot_nt = opt_young_nt ? 1u : 0u;
             const uint32_t yg = (uint32_t)std::max<uint64_t>(
                 1, std::min<uint64_t>(((uint64_t)(v1 - v0) + 3) / 4,
                                       opt_young_grid > 0 ? (uint64_t)opt_young_grid : pull_grid_cap(nt_rows, opt_pull_grid)));
@@ -2605,6 +2607,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_pull_tile_order = env_option("GOSSIP_PULL_TILE_ORDER", 1);
         e->opt_young_waves = env_option("GOSSIP_YOUNG_WAVES", 4);
         e->opt_young_own = env_option("GOSSIP_YOUNG_OWN", 0);
+        e->opt_young_nt = env_option("GOSSIP_YOUNG_NT", 1);
         e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
         e->opt_xchunks = env_option("GOSSIP_XCHUNKS", 4);
         e->opt_late_age = env_option("GOSSIP_LATE_AGE", -1);
@@ -2933,6 +2936,9 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     } else if (k == "pull_gate") {
         if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "pull_gate: 0 or 1");
         e->opt_pull_gate = value;
+    } else if (k == "young_nt") {
+        if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "young_nt: 0 or 1");
+        e->opt_young_nt = value;
     } else if (k == "young_own") {
         if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "young_own: 0 or 1");
         e->opt_young_own = value;

@@ -97,6 +97,7 @@ struct YoungArgs {
     // write index was w (0xff: none); n2 = entries of t-2's write list (0: slot_next is stale).
     const uint8_t* map2;
     uint32_t own, n2;
+    uint32_t slot_nt;  // option young_nt: non-temporal slot-line loads (C4 shard, young alone 21.1 -> 19.0 ms)
 };
 
 constexpr uint32_t kYoungSpare = 32;  // spare accumulator words per wave (tombstones land here)
@@ -212,8 +213,15 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                     q2[k] = make_ulonglong2(~0ull, ~0ull);
                     if (p < 64u && u != 0xffffffffu) {
                         const uint16_t* sl = a.slot_cur + (uint64_t)(u & 0x7fffffffu) * kSlotU16 + (lane & 7u) * 8u;
-                        q[k] = *reinterpret_cast<const ulonglong2*>(sl);
-                        if (u & 0x80000000u) q2[k] = *reinterpret_cast<const ulonglong2*>(sl + 64u);
+                        // (option young_nt: peers' slot lines are read once per reader and never
+                        // reused from the caches -- non-temporal, like k_pull's rows)
+                        if (a.slot_nt) {
+                            q[k] = load_row16<true>(reinterpret_cast<const uint64_t*>(sl));
+                            if (u & 0x80000000u) q2[k] = load_row16<true>(reinterpret_cast<const uint64_t*>(sl + 64u));
+                        } else {
+                            q[k] = *reinterpret_cast<const ulonglong2*>(sl);
+                            if (u & 0x80000000u) q2[k] = *reinterpret_cast<const ulonglong2*>(sl + 64u);
+                        }
                     }
                 }
             };
