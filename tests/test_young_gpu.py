@@ -120,16 +120,17 @@ def test_young_periodic_snapshots(gossip, oracle, monkeypatch):
     assert got == [tuple(x) for x in ref.periodic]
 
 
-@pytest.mark.parametrize("overlap", [0, 1, 2])
-def test_young_off_equals_on(gossip, overlap):
+@pytest.mark.parametrize("overlap,nt", [(0, 1), (1, 1), (2, 1), (1, 0)])
+def test_young_off_equals_on(gossip, overlap, nt):
     # 200k nodes (below the auto threshold): forced on == forced off, collisions included, with
-    # k_pull_young after k_pull (0) or concurrent on a second stream (1: launched first, 2: second)
+    # k_pull_young after k_pull (0) or concurrent on a second stream (1: launched first, 2: second),
+    # its slot lines read non-temporally (young_nt 1, the default) or cached
     n = 200_000
     topo = gossip.Topology.gnp(n, 16.0 / (n - 1), 79, gossip.TOPO_SKIP, threads=16)
     t_cut = gossip.seconds_to_ns(5.2)
     ev = gossip.make_schedule(n, 80, T0, t_cut, id_mask=0xFFFFF)
     lat = gossip.milliseconds_to_ns(5.0)
-    on = _run(gossip, topo, ev, lat, t_cut, dict(young=1, young_overlap=overlap), flags=gossip.F_TIMING)
+    on = _run(gossip, topo, ev, lat, t_cut, dict(young=1, young_overlap=overlap, young_nt=nt), flags=gossip.F_TIMING)
     off = _run(gossip, topo, ev, lat, t_cut, dict(young=0))
     a, b = on.stats(), off.stats()
     c = on.counters()
