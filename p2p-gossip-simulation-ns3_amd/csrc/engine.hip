@@ -203,10 +203,12 @@ int64_t env_option(const char* name, int64_t dflt) {
 // Cap on the pull's blocks per launch (4 waves each, striding over 64-node chunks).  Measured
 // (profiles/r01/grid_ab.jsonl, grid_ab2.jsonl): non-temporal (> 16 GiB) bitmaps like finer
 // work units -- C4 121.4 -> 119.5 ms per launch at 16,384 blocks, its 8-rank share 37.3 -> 36.3
-// ms -- while cache-resident ones keep 2,048 (C3 2.91 ms vs 3.06 ms at 16,384).
+// ms -- while cache-resident ones kept 2,048 (C3 2.91 ms vs 3.06 ms at 16,384).  Round 3, with
+// 5 waves per SIMD: C3 2.64 ms at 2,048, 2.55 at 4,096, 2.55 at 8,192, 2.69 at 1,024 blocks
+// (profiles/r03/ab/r3c3_*), so cache-resident bitmaps get 4,096.
 uint64_t pull_grid_cap(bool nt, int64_t ov) {
     if (ov > 0) return (uint64_t)ov;
-    return nt ? 16384ull : 2048ull;
+    return nt ? 16384ull : 4096ull;
 }
 
 // Word-lanes per node of the sparse pull for windows wider than 64 words.  32 lanes (passes of
