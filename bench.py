@@ -188,6 +188,10 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
         acc["nt"], acc["grid"] = c1.pull_nt, c1.pull_grid
         acc["late_age"] = c1.pull_late_age
         acc["pull_tiles"] = c1.pull_tiles
+        acc["lpw"], acc["pull_sat"] = c1.pull_lpw, c1.pull_sat
+        acc["dense_tiles"] = max(acc.get("dense_tiles", 0), c1.pull_dense_tiles)
+        acc["sat_skips"] = acc.get("sat_skips", 0) + c1.pull_sat_skips - c0.pull_sat_skips
+        acc["early_retires"] = acc.get("early_retires", 0) + c1.window_early_retires
         acc["ramp_ticks"] = c0.ticks
         if rank == 0:
             log(f"[bench] shard {s} of {shards}: {c1.edge_events - c0.edge_events} edge events in "
@@ -329,6 +333,7 @@ def main():
     # Shards: at least what one GPU's HBM needs, at least one per rank, a multiple of the ranks;
     # doubled (on every rank) when any rank's engine runs out of device memory.
     passes = max(1, -(-wl["fit_shards"] // world))
+    retried = []  # share-shard counts that did not fit (GOSSIP_ECAPACITY / ENOMEM), in order
     while True:
         shards = passes * world
         my_shards = [rank * passes + q for q in range(passes)]
@@ -348,6 +353,7 @@ def main():
             break
         if rank == 0:
             log(f"[bench] {shards} shards do not fit ({err or 'another rank'}): retrying with {2 * shards}")
+        retried.append(shards)
         passes *= 2
     layout = (f"{shards} share shards, {len(my_shards)} per GPU in sequence" if len(my_shards) > 1
               else f"{shards} share shards, one per GPU")
@@ -403,9 +409,11 @@ def main():
                 "slice_schedule": sinfo,
                 "edge_events_timed": edges_total,
                 "share_shards": shards,
+                "shards_retried": retried,
                 "shards_per_gpu": len(my_shards),
                 "live_words_per_node": acc["words_hw"],
                 "window_capacity_words": acc["words_cap"],
+                "window_early_retires": acc.get("early_retires", 0),
                 "device_gib": acc["dev_bytes"] / 2**30,
                 "parallelism": f"share-shard x{shards} over {max(world, 1)} rank(s)",
             },
@@ -433,14 +441,18 @@ def main():
                 "own_seen_read": per_launch(16 * acc["srd"]),
                 "own_seen_write": per_launch(16 * acc["swr"]),
                 "frontier_write": per_launch(16 * acc["fwr"]),
-                "per_node_rowptr_counters_occupancy": per_launch(
+                "per_node_rowptr_counters_occupancy_sat": per_launch(
                     acc["moved"] - 16 * acc["pe"] - 4 * acc["col"] - 8 * acc["nz"] -
                     16 * (acc["srd"] + acc["swr"] + acc["fwr"])),
             },
+            "saturated_tiles_skipped_per_launch": per_launch(acc.get("sat_skips", 0)),
+            "dense_row_tiles_last_tick": acc.get("dense_tiles", 0),
         }
         variant = {"nt_rows": acc["nt"], "grid": acc["grid"],
                    "young_overlap": YOUNG_OVERLAP if acc["young_launches"] else None,
-                   "late_age": acc.get("late_age", 0), "pull_tiles": acc.get("pull_tiles", 0)}
+                   "late_age": acc.get("late_age", 0), "pull_tiles": acc.get("pull_tiles", 0),
+                   "lanes_per_node": acc.get("lpw", 0), "pull_sat": acc.get("pull_sat", 0),
+                   "dense_rows": 1 if acc.get("dense_tiles", 0) else 0}
         t_pull, why_pull = pmc_traffic(wl["name"], out, variant)
         k_pull["traffic"] = t_pull
         young = None

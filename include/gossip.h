@@ -209,8 +209,10 @@ int gossip_engine_connect_rccl(gossip_engine* e, const uint8_t* unique_id, uint3
 /* Abort the engine's RCCL communicator (ncclCommAbort).  The one call that may be made from
  * another thread while the engine is inside gossip_engine_run: when one rank of a partition
  * fails, its peers are blocked in a collective that can never complete; aborting their
- * communicators makes their gossip_engine_run return GOSSIP_EHIP instead of hanging.  A no-op
- * without a communicator; the engine is then only good for gossip_engine_destroy. */
+ * communicators makes their gossip_engine_run return GOSSIP_EHIP instead of hanging.  The
+ * engine is then only good for gossip_engine_destroy: every later step (gossip_engine_run,
+ * group_run, tick_begin) and every collective its thread would still issue returns
+ * GOSSIP_ESTATE, with or without a communicator. */
 int gossip_engine_abort(gossip_engine* e);
 /* Lockstep backend: the ranks' engines must all be on ONE device (the unpack reads the other
  * ranks' messages in place; no peer access is enabled). */
@@ -275,15 +277,18 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *                                                                          [GOSSIP_YOUNG_CAP]
  *   "pull_gate"        1: k_pull skips the own-seen loads of tiles no peer holds a row of (the
  *                      default), 0: reads every live pair                     [GOSSIP_PULL_GATE]
+ *   "pull_sat"         1: k_pull keeps a saturation bit per (node, tile) -- every live column of
+ *                      the tile seen -- and skips saturated tiles until a birth lands in them
+ *                      (default), 0: off                                       [GOSSIP_PULL_SAT]
+ *   "dense_rows"       tiles whose frontier rows are expected dense everywhere are written whole
+ *                      (zeros included) and read the next tick without occupancy words: -1 auto
+ *                      (BFS layer model of the graph, default), 0 off, 1 every listed tile
+ *                      (tests)                                                [GOSSIP_DENSE_ROWS]
  *   "young_grid"       k_pull_young blocks, 0 = the pull grid                [GOSSIP_YOUNG_GRID]
- *   "young_waves"      k_pull_young register budget in waves per SIMD: 4 (no spills), 5, 6
- *                                                                         [GOSSIP_YOUNG_WAVES]
+ *   "young_list_cap"   seen-list entries per node (1..127, default 127): beyond it a list overflows
+ *                      to dense seen rows (tests: small lists exercise the overflow paths)
  *   "young_nt"         1: k_pull_young reads its peers' slot lines non-temporally (default), 0:
  *                      cached                                                  [GOSSIP_YOUNG_NT]
- *   "young_own"        1: k_pull_young dedups a node's incoming bits against its own frontier
- *                      of the last two ticks (its own slots, read with the peers'), reading
- *                      seen only for id-group words and overflowed nodes; 0: against its seen
- *                      words (default: measured faster on C4)                 [GOSSIP_YOUNG_OWN]
  *   "young_overlap"    0: k_pull_young after k_pull on the engine stream; 1: the two run
  *                      concurrently on two streams, k_pull_young launched first (default);
  *                      2: concurrently, k_pull launched first; 3 / 4: as 1 with the second
@@ -371,8 +376,17 @@ typedef struct gossip_counters {
     uint64_t young_line2_misses; /* second slot lines fetched without a hint (k_pull_young) */
     uint32_t pull_late_age;      /* late_age in effect for the last pull (0: no early exit) */
     uint32_t pull_tiles;         /* 1: the last tick's k_pull passes ran over tile lists (option pull_tiles) */
-    uint64_t young_fresh_lines;  /* seen lines of fresh tiles cleared by k_pull_young [128 B]; in
-                                    young_bytes_moved */
+    uint64_t young_fresh_lines;  /* seen rows k_pull_young wrote whole [128 B]: materialised from the
+                                    seen lists of tiles leaving the young set, and fresh tiles cleared
+                                    at nodes whose list overflowed; in young_bytes_moved */
+    uint32_t pull_lpw;           /* word-lanes per node of the last k_pull launch (32: k_pull<32,1>) */
+    uint32_t pull_dense_tiles;   /* tiles the last tick's k_pull read as dense rows (option dense_rows) */
+    uint64_t pull_sat_skips;     /* (node, tile) items k_pull skipped as saturated since reset (pull_sat) */
+    uint32_t pull_sat;           /* 1: the last tick's k_pull kept saturation bits (option pull_sat) */
+    uint32_t pad0;
+    uint64_t window_early_retires; /* allocations that first retired tiles from the last tick's
+                                      liveness (the window near its capacity) since creation */
+    uint64_t young_list_lines;   /* seen-list lines k_pull_young read and wrote [128 B] since reset */
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 /* Option rehearse_rows = R: per row block r < R, summed since the last reset_timing -- pull time,

@@ -74,6 +74,7 @@ struct Birth {
     uint32_t poff;   // group: offset of member phases in the per-tick phase buffer
     uint32_t flags;  // BF_*
     uint32_t widx;   // write-sparse index of the birth's tile this tick (0xff: dense tile)
+    uint32_t yid;    // young id of that tile (its seen-list entries, young_kernel.h)
 };
 
 struct PullArgs {
@@ -115,6 +116,11 @@ struct PullArgs {
     // entries lies in one occupancy word.  Null: consecutive tiles.
     const uint16_t* ptile = nullptr;
     uint32_t nptile = 0;
+    // Saturated tiles and dense-row tiles (k_pull<LPW,1> over tile lists; pull_kernel.h): per node
+    // and occupancy word, bit (tile & 63) = every live column of the tile is in the node's seen
+    // words (null: off); tmask[TM_WORDS * tw + TM_*] the tick's per-occupancy-word tile masks.
+    unsigned long long* sat = nullptr;
+    const unsigned long long* tmask = nullptr;
 };
 
 // Phase-ordered update of id groups inside one word (rare: only words holding groups).
@@ -143,7 +149,7 @@ __device__ __forceinline__ uint64_t group_fix(uint64_t nw, uint64_t seen, uint64
 // separate 128-B lines and summed on the host.  Every wave adds its own counts at its end; with a
 // single copy, thousands of waves finishing together queue their atomics on ONE L2 line and wait
 // for them at the next barrier (k_dense_dedup: 4,096 waves x 3 atomics = ~100 us per C2 dispatch).
-constexpr uint32_t kAcctSlots = 16, kAcctReplicas = 64;
+constexpr uint32_t kAcctSlots = 32, kAcctReplicas = 64;
 __device__ __forceinline__ void acct_add(unsigned long long* acct, uint32_t slot, unsigned long long v) {
     atomicAdd(&acct[(blockIdx.x & (kAcctReplicas - 1u)) * kAcctSlots + slot], v);
 }
@@ -287,7 +293,31 @@ struct BirthArgs {
     const int32_t* rev;
     uint8_t* hint_next;
     uint32_t stamp_next;
+    uint16_t* list;            // young tiles: seen lists (young_kernel.h)
+    const uint8_t* wt_yid;     // write-sparse index -> young id, this tick
+    uint32_t list_max;         // entries a list holds (kListU16 - 1; option young_list_cap)
 };
+
+// Seen-list entries [lo, hi] of node list ls in young id yid, word wit (bits of word w)
+__device__ uint64_t list_word_bits(const uint16_t* ls, uint32_t lo, uint32_t hi, uint32_t yid, uint32_t wit) {
+    uint64_t r = 0ull;
+    for (uint32_t k = lo; k <= hi; k++) {
+        const uint32_t e = ls[k];
+        if (e != kSlotTomb && (e >> 10) == yid && ((e >> 6) & 15u) == wit) r |= 1ull << (e & 63u);
+    }
+    return r;
+}
+
+// A seen list that cannot take a birth's entries: its entries become the dense seen rows of the
+// tiles young next tick (this tick's write-sparse ones), and the header says so (young_kernel.h)
+__device__ void list_spill(const BirthArgs& a, uint64_t v, uint16_t* ls) {
+    const uint32_t tot = ls[0] & 127u;
+    for (uint32_t q = 0; q < a.nwt; q++) {
+        uint64_t* row = a.seen + v * a.stride + (uint64_t)a.wt[q] * 16u;
+        for (uint32_t k = 0; k < 16; k++) row[k] = list_word_bits(ls, 1, tot, a.wt_yid[q], k);
+    }
+    ls[0] = (uint16_t)kListOverflow;
+}
 
 // Young-tile slot of a birth's node: the arrival bits of the group mask gm in word w (from the
 // slot entries; k_pull_young wrote them this tick), optionally tombstoning those entries.
@@ -341,15 +371,21 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
     uint64_t* fp = a.Fnext + v * a.stride + w;
     uint64_t* sp = a.seen + v * a.stride + w;
     if (x.widx != 0xffu && a.slot) {
-        // young tile (young_kernel.h): F_next of this node is its slot, unless overflowed
+        // young tile (young_kernel.h): F_next of this node is its slot, unless overflowed; its
+        // processedShares bits are in its seen list, unless that overflowed
         uint16_t* s = a.slot + v * kSlotU16;
         uint32_t hdr = s[0];
         const bool ovf = hdr == kSlotOverflow;
+        uint16_t* ls = a.list + v * kListU16;
+        const uint32_t lh = ls[0];
+        const bool lovf = lh == kListOverflow;
         bool eff = true;
+        uint64_t arr = 0ull;
+        const uint64_t gm = x.kind == BIRTH_GROUP ? (x.glen >= 64 ? ~0ull : ((1ull << x.glen) - 1ull)) << x.glo : 0ull;
         if (x.kind == BIRTH_GROUP) {
-            const uint64_t gm = (x.glen >= 64 ? ~0ull : ((1ull << x.glen) - 1ull)) << x.glo;
-            const uint64_t arr = ovf ? (*fp & gm) : slot_word_bits(s, hdr, x.widx, w & 15u, gm, false);
-            const uint64_t prior = (*sp & gm) & ~arr;
+            arr = ovf ? (*fp & gm) : slot_word_bits(s, hdr, x.widx, w & 15u, gm, false);
+            // (the list's entries up to `kept` predate this tick; this tick's arrivals follow)
+            const uint64_t prior = lovf ? (*sp & gm) & ~arr : list_word_bits(ls, 1, lh >> 7, x.yid, w & 15u) & gm;
             if (prior) {
                 eff = false;
             } else if (arr) {
@@ -383,7 +419,22 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
                         if (a.rev[j] >= 0) a.hint_next[a.rev[j]] = (uint8_t)a.stamp_next;
             }
         }
-        *sp |= bit;
+        if (lovf) {
+            *sp |= bit;
+        } else {
+            // the list takes the bit -- a group's every bit (lists hold whole groups), unless this
+            // tick's arrival of the group already put them there
+            const uint64_t add = x.kind == BIRTH_GROUP ? (arr ? 0ull : gm) : bit;
+            uint32_t tot = lh & 127u;
+            if (tot + (uint32_t)__popcll(add) > a.list_max) {
+                list_spill(a, v, ls);
+                *sp |= add;
+            } else {
+                for (uint64_t m = add; m; m &= m - 1ull)
+                    ls[1 + tot++] = (uint16_t)((x.yid << 10) | ((w & 15u) << 6) | (uint32_t)__builtin_ctzll(m));
+                ls[0] = (uint16_t)list_header(lh >> 7, tot);
+            }
+        }
         a.effgen[v] += 1u;
         atomicOr(&a.live[w], (unsigned long long)bit);
         if (a.snap && x.phase < a.snap_r) atomicAdd(a.snap, 1ull);
@@ -496,7 +547,8 @@ struct YoungPack {
     YoungTile yt[kYoungMax];  // k_pull_young's tiles, sorted by tile
     uint32_t wt[64];          // write-sparse index -> tile (births, spills)
     uint8_t lv[kYoungMax];    // positions in yt of the leaving tiles, by tile
-    uint8_t map2[64];         // t-2's write index -> read position of the same tile (0xff: none)
+    uint8_t ymap[64];         // young id -> position in yt (0xff: none): seen-list entries
+    uint8_t wt_yid[64];       // write-sparse index -> young id (births' list spills)
 };
 
 constexpr int kRing = 4;   // host staging slots
@@ -643,9 +695,30 @@ struct gossip_engine {
     uint64_t ptile_cap = 0;
     std::vector<uint32_t> pt_off, pt_cnt;  // per launch window of this tick
     bool pt_used = false;                  // the last tick's k_pull ran over tile lists
-    int64_t opt_young_waves = 4;      // k_pull_young register budget: waves per SIMD (4, 5, 6)
-    int64_t opt_young_own = 0;        // k_pull_young dedups against the node's own last two frontiers
+    // Saturated tiles and dense-row tiles (pull_kernel.h; options pull_sat, dense_rows)
+    int64_t opt_pull_sat = 1;              // 1: k_pull keeps and trusts per-node saturation bits
+    int64_t opt_dense_rows = -1;           // -1 auto (BFS layer model), 0 off, 1 every listed tile
+    unsigned long long* d_sat = nullptr;   // n x ntw words
+    unsigned long long* h_tmask[kRing] = {};
+    unsigned long long* d_tmask[kRing] = {};
+    uint32_t tmask_cap = 0;                // words per slot
+    bool sat_used = false;                 // this tick's k_pull keeps saturation bits
+    std::vector<int64_t> tile_listed;      // last tick a tile was in k_pull's lists
+    std::vector<int64_t> tile_dw;          // last tick every node's F_next row of the tile was written
+    std::vector<int64_t> tile_inj_prev;    // the injection tick before tile_last_inject
+    std::vector<uint32_t> tile_cols;       // columns allocated in the tile (this life)
+    std::vector<double> hop_front;         // expected frontier fraction per hop (BFS layer model)
+    uint32_t last_lpw = 0, last_dense_tiles = 0;
+    uint64_t sat_launches = 0;
+    bool dense_row_hop(uint32_t tl, int64_t hop) const;
+    void mark_inject(uint32_t tl, int64_t t) {
+        if (tile_last_inject[tl] != t) {
+            tile_inj_prev[tl] = tile_last_inject[tl];
+            tile_last_inject[tl] = t;
+        }
+    }
     int64_t opt_young_nt = 1;         // k_pull_young reads peers' slot lines non-temporally
+    int64_t opt_young_list_cap = kListU16 - 1;  // seen-list entries (tests: small lists overflow)
     int64_t opt_late_age = -1;        // k_pull early exit for tiles >= this many ticks old (0: off, -1: auto)
     int64_t late_age_now() const {    // auto: every tile of a gathering (CSR) pull
         return opt_late_age >= 0 ? opt_late_age : dense ? 0 : kAutoLateAge;
@@ -664,13 +737,14 @@ struct gossip_engine {
     std::vector<int64_t> tile_first;           // tick of a tile's first birth
     std::vector<uint8_t> tile_widx;            // write-sparse index of the last tick (0xff: none)
     std::vector<uint32_t> wt_last;             // write-sparse index -> tile of the last tick
-    std::vector<uint32_t> wt_last2;            // ... and of the tick before (own-frontier dedup)
+    std::vector<uint8_t> tile_yid;             // young id of a young tile (kYidNone: not young)
+    uint64_t yid_used = 0;                     // young ids in use (0 .. 62)
+    uint16_t* d_ylist = nullptr;               // n x kListU16 seen lists (young_kernel.h)
     YoungPack* h_young[kRing] = {};
     YoungPack* d_young[kRing] = {};
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers_young;
     double young_ms_done = 0.0;
     uint64_t young_launches = 0;
-    uint64_t young_fresh_lines = 0;  // fresh tiles' seen lines k_pull_young cleared (128 B each)
     // ---- timing / counters
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers;
     std::vector<hipEvent_t> event_pool;
@@ -757,6 +831,9 @@ struct gossip_engine {
     void rehearse_harvest();
     int ensure_xstream();
     int retire_from(int64_t known_tick, const unsigned long long* live);
+    int retire_early(int64_t t);
+    uint32_t soft_cap() const;
+    uint64_t early_retires = 0;  // ticks whose allocation waited for the last tick's liveness
     int alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t);
     int grow(uint32_t new_stride);
     uint32_t grows = 0;
@@ -776,14 +853,15 @@ gossip_engine::~gossip_engine() {
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
     hipFree(d_rowptr_c); hipFree(d_col_c); hipFree(d_degc);
     for (int k = 0; k < 4; k++) { hipFree(d_smask[k]); hipHostFree(h_smask[k]); }
-    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen_mem); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
+    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen_mem); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_sat); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     hipFree(d_msg); hipFree(d_cnt); hipFree(d_scan_tmp); hipFree(d_recv_msgs); hipFree(d_sizes);
     hipFree(d_tot); hipFree(d_ovf); hipHostFree(h_tot);
     for (int k = 0; k < kRing; k++) { hipFree(d_ptile[k]); hipHostFree(h_ptile[k]); }
+    for (int k = 0; k < kRing; k++) { hipFree(d_tmask[k]); hipHostFree(h_tmask[k]); }
     hipFree(d_slot[0]); hipFree(d_slot[1]);
-    hipFree(d_rev); hipFree(d_hint[0]); hipFree(d_hint[1]);
+    hipFree(d_rev); hipFree(d_hint[0]); hipFree(d_hint[1]); hipFree(d_ylist);
     for (int k = 0; k < kRing; k++) { hipFree(d_young[k]); hipHostFree(h_young[k]); }
     for (auto& p : timers_young) {
         hipEventDestroy(p.first);
@@ -1018,7 +1096,7 @@ int gossip_engine::alloc_device() {
         young = ok && (opt_young == 1 || (opt_young == -1 && n >= (1u << 20) && est_entries >= kYoungMinEntries));
     }
     // slots, plus the second-line hints (young_kernel.h): reverse-edge index + 2 hint bytes per entry
-    const uint64_t slot_bytes = young ? 2ull * n * kSlotU16 * 2u + nnz * 6u : 0ull;
+    const uint64_t slot_bytes = young ? 2ull * n * kSlotU16 * 2u + (uint64_t)n * kListU16 * 2u + nnz * 6u : 0ull;
     size_t freeb = 0, totalb = 0;
     HIP_TRY(hipMemGetInfo(&freeb, &totalb));
     if (opt_mem_limit > 0) {  // a memory budget below the device's (tests, co-located engines)
@@ -1036,7 +1114,7 @@ int gossip_engine::alloc_device() {
         // 20-tick slice measured 1,200 words estimated and more needed.
         const uint64_t want = stride + std::max<uint64_t>(stride / 4, 2 * kTileWords);
         const uint64_t other = (uint64_t)n * 24 + nnz * 4 + ((uint64_t)n + 1) * 8 + slot_bytes +
-                               16ull * n * ((want + 1023u) / 1024u) + (4ull << 30);  // + RCCL / context
+                               24ull * n * ((want + 1023u) / 1024u) + (4ull << 30);  // + RCCL / context (24: nz x 2 + sat)
         const uint64_t per_word = 3ull * n * 8 + (dense ? 8ull * n_pad : 0ull);
         uint64_t fit = freeb > other ? ((uint64_t)freeb - other) / per_word : 0ull;
         fit = fit / kTileWords * kTileWords;
@@ -1056,6 +1134,7 @@ int gossip_engine::alloc_device() {
     seen_n = row_count > 1 ? v1 - v0 : n;
     const uint64_t bm_seen = (uint64_t)seen_n * stride * 8;
     const uint64_t need = 2 * bm + bm_seen + (uint64_t)n * 24 + (nnz * 4) + ((uint64_t)n + 1) * 8 + slot_bytes +
+                          24ull * n * ((stride + 1023u) / 1024u) +
                           (dense ? (uint64_t)stride * 8 * n_pad : 0ull);
     if (need > (uint64_t)freeb)
         return set_error(GOSSIP_ENOMEM, "device memory: need " + std::to_string(need) +
@@ -1074,6 +1153,21 @@ int gossip_engine::alloc_device() {
         for (int k = 0; k < 2; k++) {
             HIP_TRY(hipMalloc(&d_nz[k], nzb));
             HIP_TRY(hipMemsetAsync(d_nz[k], 0, nzb, stream));
+        }
+        if (!dense) {  // saturation bits (k_pull over tile lists)
+            HIP_TRY(hipMalloc(&d_sat, nzb));
+            HIP_TRY(hipMemsetAsync(d_sat, 0, nzb, stream));
+        }
+    }
+    {  // BFS layer model for the dense-row tiles: frontier fraction per hop of one flood
+        hop_front.clear();
+        const double avg_deg = n ? (double)nnz / n : 0.0;
+        double reached = n ? 1.0 / n : 0.0, front = reached;
+        for (int h = 0; h < 64 && front > 0.0; h++) {
+            hop_front.push_back(front);
+            const double nx = (1.0 - reached) * (1.0 - std::exp(-avg_deg * front));
+            reached += nx;
+            front = nx;
         }
     }
     HIP_TRY(hipMalloc(&d_recv, (size_t)n * 4));
@@ -1131,6 +1225,11 @@ int gossip_engine::alloc_device() {
             HIP_TRY(hipMalloc(&d_young[k], sizeof(YoungPack)));
             HIP_TRY(hipHostMalloc(&h_young[k], sizeof(YoungPack), hipHostMallocDefault));
         }
+        // empty seen lists: header 0, every entry a tombstone
+        HIP_TRY(hipMalloc(&d_ylist, (size_t)n * kListU16 * 2u));
+        HIP_TRY(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(d_ylist), (unsigned short)kSlotTomb,
+                                  (size_t)n * kListU16, stream));
+        HIP_TRY(hipMemset2DAsync(d_ylist, kListU16 * 2u, 0, 2, n, stream));
     }
     const uint32_t bcap = std::max<uint32_t>(max_births, 1);
     const uint32_t pcap = std::max<uint32_t>(max_group_phases, 1);
@@ -1147,7 +1246,7 @@ int gossip_engine::alloc_device() {
         HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&live_done[k], hipEventDisableTiming));
     }
-    device_bytes = 2 * bm + bm_seen + 16ull * n * ntw + (uint64_t)n * 20 + nnz * 4 + ((uint64_t)n + 1) * 8 + 2ull * stride * 8 + slot_bytes +
+    device_bytes = 2 * bm + bm_seen + (d_sat ? 24ull : 16ull) * n * ntw + (uint64_t)n * 20 + nnz * 4 + ((uint64_t)n + 1) * 8 + 2ull * stride * 8 + slot_bytes +
                    kRing * ((uint64_t)stride * sizeof(WordCtl) + (uint64_t)bcap * sizeof(Birth) + pcap * 4);
     if (dense) {
         const uint64_t ft = (uint64_t)stride * 8 * n_pad;
@@ -1168,6 +1267,11 @@ int gossip_engine::alloc_device() {
     tile_last_inject.assign(stride / kTileWords, INT64_MIN);
     tile_first.assign(stride / kTileWords, INT64_MIN);
     tile_widx.assign(stride / kTileWords, 0xffu);
+    tile_yid.assign(stride / kTileWords, (uint8_t)kYidNone);
+    tile_listed.assign(stride / kTileWords, INT64_MIN);
+    tile_dw.assign(stride / kTileWords, INT64_MIN);
+    tile_inj_prev.assign(stride / kTileWords, INT64_MIN);
+    tile_cols.assign(stride / kTileWords, 0u);
     word_insts.assign(stride, {});
     col_phase.assign((size_t)stride * 64, 0);
     col_src.assign((size_t)stride * 64, UINT32_MAX);
@@ -1190,6 +1294,7 @@ int gossip_engine::grow(uint32_t new_stride) {
         // exchange.
         int* d_ok = reinterpret_cast<int*>(d_scalars);  // scratch word [0]
         HIP_TRY(hipMemcpyAsync(d_ok, &ok, sizeof(int), hipMemcpyHostToDevice, stream));
+        if (aborted.load()) return set_error(GOSSIP_ESTATE, "RCCL: the row partition was aborted");
         if (ncclAllReduce(d_ok, d_ok, 1, ncclInt32, ncclMin, comm, stream) != ncclSuccess)
             return set_error(GOSSIP_EHIP, "RCCL: capacity agreement failed");
         HIP_TRY(hipMemcpyAsync(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost, stream));
@@ -1245,6 +1350,12 @@ int gossip_engine::grow(uint32_t new_stride) {
             d_nz[k] = q;
         }
         device_bytes += 16ull * n * (new_ntw - ntw);
+        if (d_sat) {  // (a cache: zeros = nothing saturated)
+            HIP_TRY(hipFree(d_sat));
+            HIP_TRY(hipMalloc(&d_sat, (size_t)n * new_ntw * 8));
+            HIP_TRY(hipMemset(d_sat, 0, (size_t)n * new_ntw * 8));
+            device_bytes += 8ull * n * (new_ntw - ntw);
+        }
         ntw = new_ntw;
     }
     int rc = 0;
@@ -1281,7 +1392,12 @@ int gossip_engine::grow(uint32_t new_stride) {
     tile_alloc.resize(new_stride / kTileWords, 0);
     tile_last_inject.resize(new_stride / kTileWords, INT64_MIN);
     tile_first.resize(new_stride / kTileWords, INT64_MIN);
+    tile_listed.resize(new_stride / kTileWords, INT64_MIN);
+    tile_dw.resize(new_stride / kTileWords, INT64_MIN);
+    tile_inj_prev.resize(new_stride / kTileWords, INT64_MIN);
+    tile_cols.resize(new_stride / kTileWords, 0u);
     tile_widx.resize(new_stride / kTileWords, 0xffu);
+    tile_yid.resize(new_stride / kTileWords, (uint8_t)kYidNone);
     word_insts.resize(new_stride);
     col_phase.resize((size_t)new_stride * 64, 0);
     col_src.resize((size_t)new_stride * 64, UINT32_MAX);
@@ -1304,6 +1420,16 @@ int gossip_engine::alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t
     }
     if (open_tile < 0 || open_bit + k > 64) {
         uint32_t tl;
+        // Near the window's capacity, retire from the last tick's liveness before widening the
+        // high-water mark: the regular retirement reads liveness kLag = 2 ticks late (the host
+        // prepares tick t while the GPU runs t - 1), so every drained tile is held two ticks past
+        // its flood; waiting here for tick t - 1 (a stall of the host's tick preparation, only on
+        // ticks that would otherwise widen the window into its last margin) frees the tiles whose
+        // floods ended a tick earlier.
+        if (free_tiles.empty() && hw + kTileWords > soft_cap()) {
+            const int rc = retire_early(t);
+            if (rc) return rc;
+        }
         if (!free_tiles.empty()) {
             tl = free_tiles.top();
             free_tiles.pop();
@@ -1318,6 +1444,9 @@ int gossip_engine::alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t
         }
         tile_alloc[tl] = 1;
         tile_first[tl] = t;
+        tile_cols[tl] = 0;  // (a new life: nothing of the previous one is trusted)
+        tile_listed[tl] = INT64_MIN;
+        tile_dw[tl] = INT64_MIN;
         for (uint32_t q = 0; q < kTileWords; q++) reset_now.push_back(tl * kTileWords + q);
         open_tile = tl;
         open_word_in_tile = 0;
@@ -1326,8 +1455,38 @@ int gossip_engine::alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t
     *word = (uint32_t)open_tile * kTileWords + open_word_in_tile;
     *lo = (uint8_t)open_bit;
     open_bit += k;
-    tile_last_inject[(uint32_t)open_tile] = t;
+    mark_inject((uint32_t)open_tile, t);
+    tile_cols[(uint32_t)open_tile] += k;
     return GOSSIP_OK;
+}
+
+// Dense-row tile (pull_kernel.h): is the tile's frontier at `hop` expected to hold a bit in every
+// node's row?  BFS layer model of the graph (alloc_device): a row of c columns at a hop whose
+// frontier covers a fraction f of the nodes holds ~c f bits; at >= kDenseRowBits an empty row is
+// improbable (e^-32), and a misjudged tile costs bytes, never results (its rows are all written).
+constexpr double kDenseRowBits = 32.0;
+bool gossip_engine::dense_row_hop(uint32_t tl, int64_t hop) const {
+    if (opt_dense_rows == 1) return hop >= 1;
+    if (hop < 0 || hop >= (int64_t)hop_front.size()) return false;
+    return (double)tile_cols[tl] * hop_front[(size_t)hop] >= kDenseRowBits;
+}
+
+// High-water mark above which alloc_bits first retires from the freshest liveness (retire_early):
+// the capacity less max(2 tiles, 1/16 of it).
+uint32_t gossip_engine::soft_cap() const {
+    const uint32_t margin = std::max<uint32_t>(2u * kTileWords, stride / 16u / kTileWords * kTileWords);
+    return stride > margin ? stride - margin : 0u;
+}
+
+int gossip_engine::retire_early(int64_t t) {
+    if (row_count > 1 || batch) return GOSSIP_OK;  // (ranks retire in lockstep; batched ticks are not timed)
+    const int64_t kt = t - 1;
+    const int ls = (int)(((kt % kRing) + kRing) % kRing);
+    if (kt < tick0 || !live_pending[ls] || live_tick[ls] != kt) return GOSSIP_OK;
+    HIP_TRY(hipEventSynchronize(live_done[ls]));
+    live_pending[ls] = false;  // (consumed: the regular step of tick t + 1 has nothing left to read)
+    early_retires++;
+    return retire_from(kt, h_live[ls]);
 }
 
 int gossip_engine::retire_from(int64_t known_tick, const unsigned long long* live) {
@@ -1421,7 +1580,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                     col_src[(size_t)w * 64 + l] = (uint32_t)q;
                 }
             }
-            tile_last_inject[I.word / kTileWords] = t;
+            mark_inject(I.word / kTileWords, t);
             b.col = I.word * 64u + I.lo + ev_rank[q];
             if (I.nsrc > 1) {
                 b.kind = BIRTH_GROUP;
@@ -1492,15 +1651,34 @@ int gossip_engine::tick_step_a(int64_t t) {
         for (uint32_t r = 0; r < ny_read; r++)
             if (YP->yt[r].flags == YT_READ) YP->lv[ny_leave++] = (uint8_t)r;
         std::sort(YP->lv, YP->lv + ny_leave, [&](uint8_t a, uint8_t b) { return YP->yt[a].tile < YP->yt[b].tile; });
-        // own-frontier dedup (young_kernel.h): where each tile of t-2's write list sits among this
-        // tick's read tiles (the same allocation: a young tile never retires while young)
-        std::memset(YP->map2, 0xff, sizeof(YP->map2));
-        for (uint32_t i = 0; i < wt_last2.size() && i < 64; i++)
-            for (uint32_t r = 0; r < ny_read; r++)
-                if (wt_last[r] == wt_last2[i] && tile_first[wt_last[r]] + 2 <= t) YP->map2[i] = (uint8_t)r;
+        // young ids (the seen lists' tile index, young_kernel.h): a fresh young tile takes the lowest
+        // free id; a tile leaving the set (or gone) gives its id back after this tick -- this
+        // tick's k_pull_young drops its entries from every list, so no list still names it
+        std::memset(YP->ymap, 0xff, sizeof(YP->ymap));
+        std::memset(YP->wt_yid, 0xff, sizeof(YP->wt_yid));
+        uint64_t yid_free_after = 0;
+        for (uint32_t q = 0; q < ny; q++) {
+            YoungTile& y = YP->yt[q];
+            uint8_t id = tile_yid[y.tile];
+            if (id == kYidNone) {  // a fresh tile
+                const uint64_t avail = ~yid_used & ((1ull << 63) - 1ull);
+                if (!avail) return set_error(GOSSIP_EHIP, "young ids exhausted");  // (<= 48 young tiles)
+                id = (uint8_t)__builtin_ctzll(avail);
+                yid_used |= 1ull << id;
+                tile_yid[y.tile] = id;
+            }
+            y.yid = id;
+            YP->ymap[id] = (uint8_t)q;
+            if (y.flags & YT_WRITE) YP->wt_yid[y.w_idx] = id;
+            else yid_free_after |= 1ull << id;  // leaving, or its tile is gone
+        }
+        for (uint32_t q = 0; q < ny; q++)
+            if ((yid_free_after >> YP->yt[q].yid) & 1ull) tile_yid[YP->yt[q].tile] = kYidNone;
+        yid_used &= ~yid_free_after;
         for (uint32_t q = 0; q < nb; q++) {
             const uint32_t tl = B[q].col >> 10;
             B[q].widx = tl < new_widx.size() ? new_widx[tl] : 0xffu;
+            B[q].yid = B[q].widx != 0xffu ? tile_yid[tl] : kYidNone;
         }
     } else {
         for (uint32_t q = 0; q < nb; q++) B[q].widx = 0xffu;
@@ -1641,6 +1819,65 @@ int gossip_engine::tick_step_a(int64_t t) {
         }
         if (at) HIP_TRY(hipMemcpyAsync(d_ptile[slot], P, (size_t)at * 2, hipMemcpyHostToDevice, stream));
     }
+    // 4c. saturation bits and dense-row tiles of k_pull (pull_kernel.h), per listed tile:
+    //   dense row (TM_DENSE): every node's F_cur row of the tile was written last tick (WF_DW by
+    //     k_pull, YT_DW by k_pull_young for a tile leaving the young set) -- read without
+    //     occupancy words;
+    //   WF_DW: the tile's F_cur at the next tick is expected dense (dense_row_hop), so k_pull
+    //     writes every node's row this tick;
+    //   sat trusted (TM_SATOK): k_pull wrote the tile's sat bits last tick (listed then, same life)
+    //     and no birth landed in it since then (a birth adds a live column the bits did not see);
+    //   TM_NZ: listed and not dense-row: the tiles that still need their peers' occupancy words.
+    // Row partitions keep neither (another rank's rows arrive only where occupied).
+    sat_used = use_ptile && opt_pull_sat != 0 && !(cfg.flags & GOSSIP_F_NOSKIP) && d_sat;
+    const bool dr_used = use_ptile && opt_dense_rows != 0 && row_count == 1 && !(cfg.flags & GOSSIP_F_NOSKIP);
+    last_dense_tiles = 0;
+    if (sat_used || dr_used) {
+        if (TM_WORDS * ntw > tmask_cap) {
+            HIP_TRY(hipStreamSynchronize(stream));
+            const uint32_t cap = TM_WORDS * std::max<uint32_t>(ntw, 8u);
+            for (int k = 0; k < kRing; k++) {
+                hipFree(d_tmask[k]);
+                hipHostFree(h_tmask[k]);
+                HIP_TRY(hipMalloc(&d_tmask[k], (size_t)cap * 8));
+                HIP_TRY(hipHostMalloc(&h_tmask[k], (size_t)cap * 8, hipHostMallocDefault));
+            }
+            tmask_cap = cap;
+        }
+        unsigned long long* TM = h_tmask[slot];
+        std::memset(TM, 0, (size_t)TM_WORDS * ntw * 8);
+        const uint32_t ntiles = hw / kTileWords;
+        for (uint32_t tl = 0; tl < ntiles; tl++) {
+            if (!tile_alloc[tl] || (WF[tl * kTileWords] & WF_YOUNG)) continue;  // not listed
+            const unsigned long long bit = 1ull << (tl & 63u);
+            unsigned long long* m = TM + (size_t)TM_WORDS * (tl >> 6);
+            const bool fresh = tile_first[tl] == t;
+            const bool dr = dr_used && !fresh && tile_dw[tl] == t - 1;
+            if (dr) {
+                m[TM_DENSE] |= bit;
+                last_dense_tiles++;
+            } else {
+                m[TM_NZ] |= bit;
+            }
+            if (sat_used && !fresh && tile_listed[tl] == t - 1 && tile_last_inject[tl] != t - 1 &&
+                tile_inj_prev[tl] != t - 1)
+                m[TM_SATOK] |= bit;
+            if (dr_used && dense_row_hop(tl, t - tile_first[tl])) {  // F_cur's hop next tick
+                for (uint32_t q = 0; q < kTileWords; q++) WF[tl * kTileWords + q] |= (uint8_t)WF_DW;
+                tile_dw[tl] = t;
+            }
+            tile_listed[tl] = t;
+        }
+        if (dr_used && young)  // tiles leaving the young set: k_pull_young writes their dense rows
+            for (uint32_t i = 0; i < ny_leave; i++) {
+                YoungTile& y = YP->yt[YP->lv[i]];
+                if (dense_row_hop(y.tile, t - tile_first[y.tile])) {
+                    y.flags |= (uint8_t)YT_DW;
+                    tile_dw[y.tile] = t;
+                }
+            }
+        HIP_TRY(hipMemcpyAsync(d_tmask[slot], TM, (size_t)TM_WORDS * ntw * 8, hipMemcpyHostToDevice, stream));
+    }
     // 5. upload + launches
     const uint32_t wact = hw;
     if (wact) HIP_TRY(hipMemcpyAsync(d_ctl[slot], C, (size_t)wact * sizeof(WordCtl), hipMemcpyHostToDevice, stream));
@@ -1672,6 +1909,9 @@ int gossip_engine::tick_step_a(int64_t t) {
         b.rowptr = d_rowptr; b.rev = d_rev;
         b.hint_next = young ? d_hint[nxt] : nullptr;
         b.stamp_next = hint_stamp(t);
+        b.list = d_ylist;
+        b.list_max = (uint32_t)opt_young_list_cap;
+        b.wt_yid = young ? d_young[slot]->wt_yid : nullptr;
         k_births<<<(cnt + 255) / 256, 256, 0, stream>>>(b);
         HIP_TRY(hipGetLastError());
         return GOSSIP_OK;
@@ -1735,6 +1975,15 @@ int gossip_engine::tick_step_a(int64_t t) {
                 if (wide_window) lpw = pull_lanes_per_node(opt_pull_lpw);
                 int epn = 1;
                 while (split_edges && !wide_window && lpw * epn * 2 <= 64 && epn * 8 < avg_deg) epn *= 2;
+                // saturation bits / dense-row tiles: the gathering kernel (EPN 1) over tile lists
+                size_t extra_lds = 0;
+                if (c.ptile && epn == 1 && (sat_used || dr_used)) {
+                    c.tmask = d_tmask[slot];
+                    c.sat = sat_used ? d_sat : nullptr;
+                    extra_lds = kPullSatLds;
+                    sat_launches += sat_used;
+                }
+                last_lpw = (uint32_t)lpw;
                 // k_pull_wide (scalar peer loop) is opt-in: on C3 it measured 3.41 ms per launch
                 // against 3.33 ms for the lane-shuffle k_pull<64,1> (profiles/r01/ab_generic.json).
                 const bool wide = split_edges && n < (1u << 24) && !(cfg.flags & GOSSIP_F_GENERIC_PULL) &&
@@ -1742,13 +1991,15 @@ int gossip_engine::tick_step_a(int64_t t) {
                 if (wide)
                     k_pull_wide<<<grid, 256, pull_lds_bytes(c.wact), stream>>>(c);
                 else
-                    launch_pull(lpw, epn, nt_rows, grid, pull_lds_bytes(c.wact, c.keep_lds != 0, c.nptile), stream, c);
+                    launch_pull(lpw, epn, nt_rows, grid, pull_lds_bytes(c.wact, c.keep_lds != 0, c.nptile) + extra_lds,
+                                stream, c);
             }
         };
         hipEvent_t e0 = nullptr, e1 = nullptr, p0 = nullptr, p1 = nullptr;
         a.inc = nullptr;
-        // DENSE phase = transpose + MFMA + dedup, each kernel timed on its own (the phase is the
-        // sum: host-side gaps between the launches of a tick are not the kernels' time)
+        // DENSE phase = transpose + MFMA + dedup, timed as ONE unit: an event before the transpose
+        // and one after the last dedup on the engine stream (a sum of per-kernel event pairs
+        // misreads 10-us kernels; the span is what the phase costs, launch gaps included)
         const bool dense_timing = dense && (cfg.flags & GOSSIP_F_TIMING);
         auto phase_begin = [&]() -> hipEvent_t {
             if (!dense_timing) return nullptr;
@@ -1760,13 +2011,13 @@ int gossip_engine::tick_step_a(int64_t t) {
             hipEvent_t y = get_event();
             if (hipEventRecord(y, stream) == hipSuccess) timers_phase.emplace_back(x, y);
         };
+        hipEvent_t dense_ph0 = nullptr;  // the DENSE phase's start (phase_end after the dedup)
         if (dense) {  // transpose the frontier to share-column bit rows (not timed as the pull)
-            hipEvent_t q = phase_begin();
+            dense_ph0 = phase_begin();
             dim3 eg(n_pad / 256u, wact);
             k_transpose<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad / 32u, wact, a.live_prev,
                                                 d_nz[fcur], ntw, d_FT);
             HIP_TRY(hipGetLastError());
-            phase_end(q);
         }
         // young tiles beside k_pull: the two kernels touch disjoint words; they share the per-node
         // counters and occupancy words, which k_pull then updates atomically (shared_out) into
@@ -1811,10 +2062,12 @@ int gossip_engine::tick_step_a(int64_t t) {
             y.cap = (uint32_t)std::min<int64_t>(kSlotU16 - 1, std::max<int64_t>(1, opt_young_cap));
             y.hint_cur = d_hint[fcur]; y.hint_next = d_hint[nxt]; y.rev = d_rev;
             y.stamp_cur = hint_stamp(t - 1); y.stamp_next = hint_stamp(t);
-            y.map2 = d_young[slot]->map2;
-            y.own = (opt_young_own && ny_read) ? 1u : 0u;
-            y.n2 = y.own ? (uint32_t)std::min<size_t>(wt_last2.size(), 64) : 0u;
             y.slot_nt = opt_young_nt ? 1u : 0u;
+            y.list = d_ylist;
+            // (k_pull_young leaves kListReserve entries of the capacity to k_births' appends)
+            y.list_cap = opt_young_list_cap > 2 * (int64_t)kListReserve ? (uint32_t)opt_young_list_cap - kListReserve
+                                                                        : (uint32_t)opt_young_list_cap / 2u;
+            y.ymap = d_young[slot]->ymap;
             const uint32_t yg = (uint32_t)std::max<uint64_t>(
                 1, std::min<uint64_t>(((uint64_t)(v1 - v0) + 3) / 4,
                                       opt_young_grid > 0 ? (uint64_t)opt_young_grid : pull_grid_cap(nt_rows, opt_pull_grid)));
@@ -1824,26 +2077,18 @@ int gossip_engine::tick_step_a(int64_t t) {
                 y1 = get_event();
                 HIP_TRY(hipEventRecord(y0, ys));
             }
-            const size_t ylds = young_lds_bytes(ny, ny_read);
-            if (opt_young_waves == 6)
-                k_pull_young<6><<<yg, 256, ylds, ys>>>(y);
-            else if (opt_young_waves == 5)
-                k_pull_young<5><<<yg, 256, ylds, ys>>>(y);
-            else
-                k_pull_young<4><<<yg, 256, ylds, ys>>>(y);
+            k_pull_young<<<yg, 256, young_lds_bytes(ny, ny_read), ys>>>(y);
             HIP_TRY(hipGetLastError());
             if (cfg.flags & GOSSIP_F_TIMING) {
                 HIP_TRY(hipEventRecord(y1, ys));
                 timers_young.emplace_back(y0, y1);
             }
             young_launches++;
-            young_fresh_lines += (uint64_t)(ny - ny_read) * (uint64_t)(v1 - v0);
             return GOSSIP_OK;
         };
         // DENSE mode: dedup of the incoming words of rows [base.v0, base.n), one node per wave
         // step, the grid sized to the rows (k_dense_dedup, dense_kernel.h)
         auto run_dedup = [&](const PullArgs& base) {
-            hipEvent_t q = phase_begin();
             const uint64_t rows = base.n > base.v0 ? base.n - base.v0 : 0;
             const uint32_t g = (uint32_t)std::max<uint64_t>(
                 1, std::min<uint64_t>((rows + kDedupWaves - 1) / kDedupWaves, 2u * (uint32_t)num_cus));
@@ -1853,7 +2098,6 @@ int gossip_engine::tick_step_a(int64_t t) {
                 c.wact = std::min(kPullLdsWords, wact - wb);
                 k_dense_dedup<<<g, 64 * kDedupWaves, pull_lds_bytes(c.wact, c.keep_lds != 0), stream>>>(c);
             }
-            phase_end(q);
         };
         // the MFMA contraction of rows [lo, hi) (DENSE mode) into the incoming words
         auto run_dense = [&](uint64_t lo, uint64_t hi) -> int {
@@ -1869,10 +2113,8 @@ int gossip_engine::tick_step_a(int64_t t) {
             while ((uint64_t)gm.mb * gm.nt * ks < min_tiles && ks * 4 <= nst) ks *= 2;
             gm.ksplit = ks;
             gm.total = gm.mb * gm.nt * ks;
-            hipEvent_t q = phase_begin();
             k_dense_bits<<<(gm.total + 7u) / 8u * 8u, 512, 0, stream>>>(gm);
             HIP_TRY(hipGetLastError());
-            phase_end(q);
             return GOSSIP_OK;
         };
         if (nchunks > 1) {
@@ -1906,6 +2148,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 if (rc) return rc;
                 if ((rc = end_chunk(c))) return rc;
             }
+            phase_end(dense_ph0);  // (row chunks: the chunks' births are inside the span)
         } else if (dense) {
             // The timed kernel in DENSE mode is the MFMA contraction (pull_ms); its incoming
             // words are then consumed by k_dense_dedup.  The whole phase -- transpose, MFMA,
@@ -1918,6 +2161,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             }
             a.inc = d_inc;
             run_dedup(a);
+            phase_end(dense_ph0);
         } else if (opt_rehearse_rows > 1 && !ny) {
             // row-partition rehearsal: one pull launch per rank's row range, each timed
             for (uint32_t r = 0; r + 1 < (uint32_t)rr_lo.size(); r++) {
@@ -1985,7 +2229,6 @@ int gossip_engine::tick_step_a(int64_t t) {
     }
     if (young) {  // F_next's slots hold this tick's write-sparse tiles: next tick reads them
         tile_widx.swap(new_widx);
-        wt_last2.swap(wt_last);
         wt_last.assign(YP->wt, YP->wt + nwt);
     }
     if (smask_any) {  // hop-batched snapshots: arrivals of this tick that precede each snapshot
@@ -2131,6 +2374,14 @@ DevLayout dev_layout(uint64_t k, uint32_t ntw, uint32_t wlive) {
     do {                                                                                    \
         ncclResult_t r_ = (x);                                                              \
         if (r_ != ncclSuccess) return set_error(GOSSIP_EHIP, std::string("RCCL: ") + ncclGetErrorString(r_)); \
+    } while (0)
+// A collective on the engine's communicator (member functions): never after gossip_engine_abort
+// freed it (another thread's abort of a failing partition), whose later calls would use freed
+// memory -- the engine then reports GOSSIP_ESTATE.
+#define COMM_TRY(x)                                                                         \
+    do {                                                                                    \
+        if (aborted.load()) return set_error(GOSSIP_ESTATE, "RCCL: the row partition was aborted"); \
+        NCCL_TRY(x);                                                                        \
     } while (0)
 
 int gossip_engine::ensure_dev(uint64_t*& p, uint64_t& cap, uint64_t words) {
@@ -2356,6 +2607,7 @@ int gossip_engine::unpack_dev(int64_t t, uint64_t lo, uint64_t hi, uint32_t wliv
 // go in a second round (re-pack, broadcast the tail, unpack), and the capacities grow to 1.25x.
 // The engine stream joins the exchange stream before the tick's liveness read-back (tick_step_b).
 int gossip_engine::exchange_rccl(int64_t t) {
+    if (aborted.load()) return set_error(GOSSIP_ESTATE, "RCCL: the row partition was aborted");
     int rc = ensure_xstream();
     if (rc) return rc;
     const uint32_t R = row_count;
@@ -2368,7 +2620,7 @@ int gossip_engine::exchange_rccl(int64_t t) {
         if ((rc = ensure_dev(d_sizes, sizes_cap, 2 * R))) return rc;
         const unsigned long long mine = nchunks;
         HIP_TRY(hipMemcpyAsync(d_sizes + row_rank, &mine, 8, hipMemcpyHostToDevice, xstream));
-        NCCL_TRY(ncclAllGather(d_sizes + row_rank, d_sizes, 1, ncclUint64, comm, xstream));
+        COMM_TRY(ncclAllGather(d_sizes + row_rank, d_sizes, 1, ncclUint64, comm, xstream));
         std::vector<unsigned long long> all(R);
         HIP_TRY(hipMemcpyAsync(all.data(), d_sizes, R * 8, hipMemcpyDeviceToHost, xstream));
         HIP_TRY(hipStreamSynchronize(xstream));
@@ -2399,19 +2651,19 @@ int gossip_engine::exchange_rccl(int64_t t) {
         geom(row_rank, c, &lo, &hi, &wl);
         HIP_TRY(hipStreamWaitEvent(xstream, ev_chunk[c], 0));
         if ((rc = pack_dev(t, lo, hi, wl, xstream))) return rc;
-        NCCL_TRY(ncclAllGather(d_msg, d_tot + (size_t)c * R, 1, ncclUint64, comm, xstream));
-        NCCL_TRY(ncclGroupStart());
+        COMM_TRY(ncclAllGather(d_msg, d_tot + (size_t)c * R, 1, ncclUint64, comm, xstream));
+        COMM_TRY(ncclGroupStart());
         for (uint32_t r = 0; r < R; r++) {
             uint64_t rlo, rhi;
             uint32_t rwl;
             geom(r, c, &rlo, &rhi, &rwl);
             const uint64_t words = dev_layout(rhi - rlo, ntw, rwl).rows + 16ull * xcap[(size_t)r * kMaxChunks + c];
             uint64_t* buf = r == row_rank ? d_msg : d_recv_msgs + at[(size_t)c * R + r];
-            NCCL_TRY(ncclBroadcast(buf, buf, words, ncclUint64, (int)r, comm, xstream));
+            COMM_TRY(ncclBroadcast(buf, buf, words, ncclUint64, (int)r, comm, xstream));
             if (r == row_rank) exchange_bytes_out += words * 8;
             else exchange_bytes_in += words * 8;
         }
-        NCCL_TRY(ncclGroupEnd());
+        COMM_TRY(ncclGroupEnd());
         for (uint32_t r = 0; r < R; r++) {
             if (r == row_rank) continue;
             uint64_t rlo, rhi;
@@ -2439,12 +2691,12 @@ int gossip_engine::exchange_rccl(int64_t t) {
             const uint64_t words = 16ull * (tot - cap);
             if (r == row_rank) {
                 if ((rc = pack_dev(t, rlo, rhi, rwl, xstream))) return rc;  // (d_msg held a later chunk)
-                NCCL_TRY(ncclBroadcast(d_msg + L.rows + 16ull * cap, d_msg + L.rows + 16ull * cap, words, ncclUint64,
+                COMM_TRY(ncclBroadcast(d_msg + L.rows + 16ull * cap, d_msg + L.rows + 16ull * cap, words, ncclUint64,
                                        (int)r, comm, xstream));
                 exchange_bytes_out += words * 8;
             } else {
                 if ((rc = ensure_dev(d_ovf, ovf_cap, words))) return rc;
-                NCCL_TRY(ncclBroadcast(d_ovf, d_ovf, words, ncclUint64, (int)r, comm, xstream));
+                COMM_TRY(ncclBroadcast(d_ovf, d_ovf, words, ncclUint64, (int)r, comm, xstream));
                 exchange_bytes_in += words * 8;
                 if ((rc = unpack_dev(t, rlo, rhi, rwl, d_recv_msgs + at[(size_t)c * R + r], d_ovf, cap, tot, false,
                                      xstream)))
@@ -2607,12 +2859,12 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_pull_gate = env_option("GOSSIP_PULL_GATE", 1);
         e->opt_pull_tiles = env_option("GOSSIP_PULL_TILES", 1);
         e->opt_pull_tile_order = env_option("GOSSIP_PULL_TILE_ORDER", 1);
-        e->opt_young_waves = env_option("GOSSIP_YOUNG_WAVES", 4);
-        e->opt_young_own = env_option("GOSSIP_YOUNG_OWN", 0);
         e->opt_young_nt = env_option("GOSSIP_YOUNG_NT", 1);
         e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
         e->opt_xchunks = env_option("GOSSIP_XCHUNKS", 4);
         e->opt_late_age = env_option("GOSSIP_LATE_AGE", -1);
+        e->opt_pull_sat = env_option("GOSSIP_PULL_SAT", 1);
+        e->opt_dense_rows = env_option("GOSSIP_DENSE_ROWS", -1);
         e->trace = (cfg->flags & GOSSIP_F_TRACE) != 0;
         e->dense = cfg->mode == GOSSIP_MODE_DENSE;
         e->handshake = (cfg->flags & GOSSIP_F_HANDSHAKE) != 0;
@@ -2763,6 +3015,8 @@ int gossip_engine_set_row_partition(gossip_engine* e, uint32_t rank, uint32_t co
     if (e->have_graph) return set_error(GOSSIP_ESTATE, "set the row partition before the graph");
     if (count == 0 || rank >= count) return set_error(GOSSIP_EINVAL, "row partition: rank >= count");
     if (e->handshake) return set_error(GOSSIP_EINVAL, "row partition: not with GOSSIP_F_HANDSHAKE");
+    if (count > 1 && e->opt_rehearse_rows > 1)  // (either order of the two calls is refused)
+        return set_error(GOSSIP_EINVAL, "row partition: not on a rehearse_rows engine");
     e->row_rank = rank;
     e->row_count = count;
     return GOSSIP_OK;
@@ -2779,7 +3033,8 @@ int gossip_rccl_unique_id(uint8_t* out, uint32_t len) {
 int gossip_engine_abort(gossip_engine* e) {
     if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
     bool expected = false;
-    if (e->comm && e->aborted.compare_exchange_strong(expected, true)) ncclCommAbort(e->comm);
+    // (the flag first: the engine's own thread checks it before every collective, COMM_TRY)
+    if (e->aborted.compare_exchange_strong(expected, true) && e->comm) ncclCommAbort(e->comm);
     return GOSSIP_OK;
 }
 
@@ -2800,6 +3055,7 @@ int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end
     for (uint32_t r = 0; r < count; r++) {
         gossip_engine* e = es[r];
         if (!e || !e->have_sched) return set_error(GOSSIP_ESTATE, "set graph and schedule first");
+        if (e->aborted.load()) return set_error(GOSSIP_ESTATE, "engine aborted (gossip_engine_abort)");
         if (e->row_count != count || e->row_rank != r) return set_error(GOSSIP_EINVAL, "engines must be ranks 0..count-1 of one partition");
         if (e->comm) return set_error(GOSSIP_EINVAL, "group run is the non-RCCL backend");
         // the unpack kernels read the other ranks' messages in place: one device only
@@ -2935,18 +3191,21 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     } else if (k == "pull_tiles") {
         if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "pull_tiles: 0 or 1");
         e->opt_pull_tiles = value;
+    } else if (k == "pull_sat") {
+        if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "pull_sat: 0 or 1");
+        e->opt_pull_sat = value;
+    } else if (k == "dense_rows") {
+        if (value < -1 || value > 1) return set_error(GOSSIP_EINVAL, "dense_rows: -1 (auto), 0 or 1");
+        e->opt_dense_rows = value;
     } else if (k == "pull_gate") {
         if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "pull_gate: 0 or 1");
         e->opt_pull_gate = value;
+    } else if (k == "young_list_cap") {
+        if (value < 1 || value > (int64_t)kListU16 - 1) return set_error(GOSSIP_EINVAL, "young_list_cap: 1 .. 127 entries");
+        e->opt_young_list_cap = value;
     } else if (k == "young_nt") {
         if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "young_nt: 0 or 1");
         e->opt_young_nt = value;
-    } else if (k == "young_own") {
-        if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "young_own: 0 or 1");
-        e->opt_young_own = value;
-    } else if (k == "young_waves") {
-        if (value < 4 || value > 6) return set_error(GOSSIP_EINVAL, "young_waves: 4, 5 or 6");
-        e->opt_young_waves = value;
     } else if (k == "young_grid") {
         if (value < 0 || value > (1 << 20)) return set_error(GOSSIP_EINVAL, "young_grid: 0 .. 2^20 blocks");
         e->opt_young_grid = value;
@@ -2981,6 +3240,7 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
 // rank's -> tick_end.
 static int check_stepping(gossip_engine* e) {
     if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    if (e->aborted.load()) return set_error(GOSSIP_ESTATE, "engine aborted (gossip_engine_abort)");
     if (!e->have_sched) return set_error(GOSSIP_ESTATE, "set graph and schedule first");
     if (e->comm) return set_error(GOSSIP_ESTATE, "host-staged stepping is not for an RCCL-connected engine");
     return GOSSIP_OK;
@@ -3232,6 +3492,7 @@ int64_t gossip_engine_current_tick(const gossip_engine* e) { return e ? e->cur :
 
 int gossip_engine_run(gossip_engine* e, int64_t tick_end) {
     if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
+    if (e->aborted.load()) return set_error(GOSSIP_ESTATE, "engine aborted (gossip_engine_abort)");
     if (!e->have_sched) return set_error(GOSSIP_ESTATE, "set graph and schedule first");
     if (e->row_count > 1 && !e->comm)
         return set_error(GOSSIP_ESTATE, "row-partitioned engine: gossip_engine_connect_rccl or gossip_engine_group_run "
@@ -3361,7 +3622,8 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     // col indices of the node passes that pulled (4 B), own-row seen reads/writes and F_next
     // writes (16 B each), row_ptr and the per-node counters.
     c->pull_bytes_moved = 16ull * acct[0] + 4ull * acct[1] + 16ull * (acct[2] + acct[3] + acct[4]) +
-                          8ull * acct[7] + e->pull_launches * (8ull * (e->n + 1) + 16ull * e->n + 8ull * e->n * e->ntw);
+                          8ull * acct[7] + e->pull_launches * (8ull * (e->n + 1) + 16ull * e->n + 8ull * e->n * e->ntw) +
+                          16ull * e->n * std::min<uint32_t>(2u, e->ntw) * e->sat_launches;  // sat words r + w
     c->pull_pair_edges = acct[0];
     c->dense_ops = acct[5];  // k_dense_gemm adds 2*M*N*K of every tile-split it computes
     c->dense_tiles_skipped = acct[6];
@@ -3412,9 +3674,16 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     c->young_line2_misses = acct[15];
     c->pull_late_age = (uint32_t)e->late_age_now();
     c->pull_tiles = e->pt_used ? 1u : 0u;
-    c->young_bytes_moved = 128ull * (acct[8] + acct[10] + acct[13] + acct[14] + acct[15] + e->young_fresh_lines) + 5ull * acct[9] +
+    c->young_bytes_moved = 128ull * (acct[8] + acct[10] + acct[13] + acct[14] + acct[15] + acct[17] + acct[18] + acct[19]) +
+                           5ull * acct[9] +
                            8ull * (acct[11] + acct[12]) + e->young_launches * (8ull * (e->n + 1) + 16ull * e->n);
-    c->young_fresh_lines = e->young_fresh_lines;
+    c->young_fresh_lines = acct[19];
+    c->young_list_lines = acct[17] + acct[18];
+    c->pull_lpw = e->last_lpw;
+    c->pull_dense_tiles = e->last_dense_tiles;
+    c->pull_sat_skips = acct[16];
+    c->pull_sat = e->sat_used ? 1u : 0u;
+    c->window_early_retires = e->early_retires;
     uint64_t g = 0;
     const uint64_t done = (uint64_t)std::max<int64_t>(0, std::min(e->cur, e->tick_end) - e->tick0);
     if (!e->tick_lo.empty()) g = e->tick_lo[std::min<uint64_t>(done, e->tick_lo.size() - 1)];
@@ -3459,7 +3728,7 @@ int gossip_engine_reset_timing(gossip_engine* e) {
     e->timers_young.clear();
     e->young_ms_done = 0.0;
     e->young_launches = 0;
-    e->young_fresh_lines = 0;
+    e->sat_launches = 0;
     for (auto& p : e->timers_phase) {
         e->event_pool.push_back(p.first);
         e->event_pool.push_back(p.second);

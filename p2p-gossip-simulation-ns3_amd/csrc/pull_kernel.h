@@ -36,6 +36,20 @@
 //                 tiles flagged WF_LATE: every tile by default, option late_age);
 //   F_next tile rows are written only when some word of the tile got a bit (and the tile's
 //   occupancy bit set); rows left unwritten hold stale bits that no reader ever loads.
+//   saturated  -- (round 4, option pull_sat) a tile whose every live column the node has seen
+//                 stays so until a birth lands in the tile (live columns only die: every
+//                 incoming bit lies in live_prev), so k_pull keeps a per-node bit per tile
+//                 (`sat`, written whole per occupancy word like nz_next) and skips the tile at
+//                 that node -- no own-seen read, no peer row, no occupancy word -- while the host
+//                 trusts the bit (tmask: listed last tick, no birth since, not re-allocated);
+//   dense rows -- (round 4, option dense_rows) tiles whose frontier rows are dense everywhere
+//                 (C4: F_cur at hops 5-7, ~100-760 bits per 1,024-share row) are read WITHOUT
+//                 occupancy words: their writer of the last tick wrote every node's row (WF_DW,
+//                 zeros included), so a peer's row is valid whatever its occupancy bit, and a
+//                 node whose other listed tiles are all saturated or dense loads no occupancy
+//                 word at all.  The random 8-B occupancy loads cost a line fetch each (C4: 282M
+//                 per shard-tick, ~36 GB of the 37 GB of k_pull traffic above its algorithmic
+//                 bytes, profiles/pmc_C4.json).
 #pragma once
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
@@ -85,7 +99,13 @@ __device__ __forceinline__ uint32_t group_add(uint32_t x, uint32_t lane) {
 
 // WF_YOUNG: the word belongs to a young tile, which k_pull_young owns this tick (young_kernel.h)
 // WF_LATE: the word's tile is old enough (option late_age) for the bottom-up early exit
-enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u, WF_YOUNG = 16u, WF_LATE = 32u };
+// WF_DW: write every node's F_next row of the tile, zeros included (its readers of the next tick
+//        read it without occupancy words: dense rows, above)
+enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u, WF_YOUNG = 16u, WF_LATE = 32u,
+                  WF_DW = 64u };
+// PullArgs::tmask, per occupancy word tw: [3 tw] dense-row tiles (read without occupancy words),
+// [3 tw + 1] tiles whose sat bits are trusted this tick, [3 tw + 2] listed tiles that need occupancy
+enum : uint32_t { TM_DENSE = 0, TM_SATOK = 1, TM_NZ = 2, TM_WORDS = 3 };
 
 constexpr uint32_t kPullLdsWords = 2048;  // words per launch: LDS liveness, new liveness, flags
 #ifndef PULL_INFLIGHT
@@ -125,6 +145,9 @@ __host__ __device__ constexpr size_t pull_lds_bytes(uint32_t wact, bool keep = f
     return (size_t)wact * 16u + (((size_t)wact + 15u) & ~(size_t)15u) + (keep ? (size_t)wact * 8u : 0u) +
            (((size_t)nptile * 2u + 15u) & ~(size_t)15u);
 }
+// + (option pull_sat) the launch's two occupancy words of tmask and every wave's sat words of its
+// 64 nodes (2 per node), behind the rest
+constexpr size_t kPullSatLds = 8u * 8u + 4u * 64u * 2u * 8u;
 constexpr uint32_t kNoWord = 0xffffffffu;
 
 // Peer ids of the first GRP peers of item k's node (0xffffffff past the list).
@@ -169,6 +192,16 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
         if (a.keep_lds) s_keep[i] = (f & WF_KEEP) ? a.ctl[a.wbase + i].keep : ~0ull;
     }
     for (uint32_t i = threadIdx.x; i < a.nptile; i += 256) s_pt[i] = a.ptile[i];
+    // saturation bits and dense-row tiles (the gathering pull over tile lists only)
+    const bool tm_on = EPN == 1 && a.tmask != nullptr && a.ptile != nullptr;  // dense rows (+ sat)
+    const bool sat_on = tm_on && a.sat != nullptr;
+    unsigned long long* s_tm = reinterpret_cast<unsigned long long*>(
+        reinterpret_cast<char*>(smem) + pull_lds_bytes(a.wact, a.keep_lds != 0, a.nptile));
+    unsigned long long* s_sat = s_tm + 8;  // [wave][node of the chunk][occupancy word of the launch]
+    if (threadIdx.x < 2u * TM_WORDS) {
+        const uint32_t twg = (a.wbase >> 10) + threadIdx.x / TM_WORDS;
+        s_tm[threadIdx.x] = (tm_on && twg < a.ntw) ? a.tmask[twg * TM_WORDS + threadIdx.x % TM_WORDS] : 0ull;
+    }
     __syncthreads();
     const uint32_t lane_id = threadIdx.x & 63u;
     // lane geometry, recomputed inside the loops from an opaque lane id (engine.hip, opaque)
@@ -210,21 +243,42 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
     };
     const uint32_t nsteps = 64u / NPW;
     unsigned long long snap_local = 0ull;
-    uint32_t t_pe = 0, t_col = 0, t_srd = 0, t_swr = 0, t_fwr = 0, t_nz = 0;  // wave-uniform
+    uint32_t t_pe = 0, t_col = 0, t_srd = 0, t_swr = 0, t_fwr = 0, t_nz = 0, t_sk = 0;  // wave-uniform
     unsigned long long nzacc = 0ull;
     const bool gather = EPN == 1;  // the pipelined id/occupancy loads
+    const uint32_t tw_base = a.wbase >> 10;  // the launch's first occupancy word
+    unsigned long long* s_satw = s_sat + (uint64_t)wave_in_block() * 128u;
+    // the trusted saturated tiles of the chunk's node idx in occupancy word tw
+    auto satv_of = [&](uint32_t idx, uint32_t tw) -> unsigned long long {
+        return sat_on ? s_satw[idx * 2u + (tw - tw_base)] : 0ull;
+    };
+    // does node idx need its peers' occupancy words of tw (some listed tile that is neither
+    // dense-row nor saturated at the node)?
+    auto nz_needed = [&](uint32_t idx, uint32_t tw) -> bool {
+        return !tm_on || (s_tm[(tw - tw_base) * TM_WORDS + TM_NZ] & ~satv_of(idx, tw)) != 0ull;
+    };
 
     for (uint64_t c0 = a.v0 + wave * 64u; npass && c0 < n; c0 += nwaves * 64u) {
         PULL_LANES
         const int64_t rp = a.rowptr[min(c0 + lane, n)];
         const int64_t rp_end = a.rowptr[min(c0 + 64u, n)];
+        if (sat_on) {  // the chunk's sat words, trusted bits only (waited for below)
+#pragma unroll
+            for (uint32_t q = 0; q < 2u; q++) {
+                const uint64_t vj = c0 + lane;
+                const uint32_t twg = tw_base + q;
+                s_satw[lane * 2u + q] = (vj < n && twg < a.ntw)
+                                            ? a.sat[vj * a.ntw + twg] & s_tm[q * TM_WORDS + TM_SATOK] : 0ull;
+            }
+        }
         // item k = (step, pass): node c0 + step * NPW + slot, the lane's word pair lw_of(pass)
         uint32_t step = 0, pass = 0;
         ulonglong2 s2c = make_ulonglong2(0ull, 0ull);
         {
             const uint64_t v = c0 + slot;
             const uint32_t lw = lw_of(0u, wl);
-            if (v < n && lw != kNoWord && (s_lp[lw] | s_lp[lw + 1u]) != 0ull)
+            if (v < n && lw != kNoWord && (s_lp[lw] | s_lp[lw + 1u]) != 0ull &&
+                !((satv_of(slot, tw_of(0u)) >> (((a.wbase + lw) >> 4) & 63u)) & 1ull))
                 s2c = load_row16<NT>(a.seen + v * stride + a.wbase + lw);
         }
         uint32_t cid0 = 0xffffffffu, cid1 = 0xffffffffu;
@@ -232,8 +286,9 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
         if (gather) {
             cid0 = pull_cid_load<LPW, EPN>(a, 0u, c0, rp, rp_end, gl, slot);
             cid1 = npass > 1u ? cid0 : pull_cid_load<LPW, EPN>(a, 1u, c0, rp, rp_end, gl, slot);
-            nz0 = cid0 != 0xffffffffu ? a.nz_cur[(uint64_t)cid0 * a.ntw + tw_of(0u)] : 0ull;
-            t_nz += wave_count(cid0 != 0xffffffffu);
+            const bool ld = cid0 != 0xffffffffu && nz_needed(slot, tw_of(0u));
+            nz0 = ld ? a.nz_cur[(uint64_t)cid0 * a.ntw + tw_of(0u)] : 0ull;
+            t_nz += wave_count(ld);
         }
         uint32_t cnt = 0;
         // Occupancy gate of the own-seen loads: nzor = OR over the node's peers of their
@@ -266,13 +321,15 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                 end = (idx + 1u < 64u) ? nxb : (int32_t)rp_end;
             }
             const uint32_t tw = tw_of(pass);  // (uniform: the pass's occupancy word)
+            // dense-row tiles of the pass's occupancy word: every peer holds a valid row (uniform)
+            const unsigned long long drm = tm_on ? s_tm[(tw - tw_base) * TM_WORDS + TM_DENSE] : 0ull;
             // ---- stage loads: own seen pair of item k+1, ids of k+2, occupancy of k+1 ----
             ulonglong2 s2n = make_ulonglong2(0ull, 0ull);
             bool s2n_gated = false;
             if (gate && nz_new) {  // (uniform) this item starts a new occupancy word
                 unsigned long long x = nz0;
                 x = group_or64<GRP>(x, lane);
-                nzor = x;
+                nzor = x | drm;
                 nz_new = false;
             }
             if (step1 < nsteps) {
@@ -288,6 +345,8 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                     // same node and occupancy word as this item, peers in one lane group
                     s2n_gated = gate && step1 == step && tw_of(pass1) == tw && e0 - b0 <= GRP &&
                                 !((nzor >> (((a.wbase + lw1) >> 4) & 63u)) & 1ull);
+                    // a saturated tile (trusted sat bit) needs nothing: not even its seen words
+                    s2n_gated |= ((satv_of(step1 * NPW + slot, tw_of(pass1)) >> (((a.wbase + lw1) >> 4) & 63u)) & 1ull) != 0ull;
                     if (!s2n_gated) s2n = load_row16<NT>(a.seen + v1 * stride + a.wbase + lw1);
                 }
             }
@@ -301,8 +360,9 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                     if (step1 == step && tw1 == tw) {
                         nz1 = nz0;  // same node, same occupancy word
                     } else {
-                        nz1 = cid1 != 0xffffffffu ? a.nz_cur[(uint64_t)cid1 * a.ntw + tw1] : 0ull;
-                        t_nz += wave_count(cid1 != 0xffffffffu);
+                        const bool ld = cid1 != 0xffffffffu && nz_needed(step1 * NPW + slot, tw1);
+                        nz1 = ld ? a.nz_cur[(uint64_t)cid1 * a.ntw + tw1] : 0ull;
+                        t_nz += wave_count(ld);
                     }
                 }
             }
@@ -317,6 +377,14 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                 lp0 = s_lp[lw];
                 lp1 = s_lp[lw + 1u];
             }
+            // a tile saturated at this node is a dead pair here: no seen read or write, nothing new
+            const unsigned long long tbit = 1ull << ((w >> 4) & 63u);
+            const bool sk = act && (satv_of(idx, tw) & tbit) != 0ull;
+            if (sk) {
+                lp0 = 0ull;
+                lp1 = 0ull;
+            }
+            t_sk += wave_count(sk && (wl & 7u) == 0u);
             const bool dead = (lp0 | lp1) == 0ull;
             ulonglong2 s2 = s2c;
             if (f0 & WF_CLEAR) s2.x = 0ull;
@@ -339,7 +407,6 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             int gneed = tn;
             gneed = (int)group_or<GRP>((uint32_t)gneed, lane);
             // ---- gather peer rows ----
-            const unsigned long long tbit = 1ull << ((w >> 4) & 63u);
             uint64_t acc0 = 0ull, acc1 = 0ull;
             if (gneed) {  // uniform inside the node group
                 const uint64_t* Fw = a.Fcur + w;
@@ -351,7 +418,8 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                     auto gchunk = [&](uint32_t cid, unsigned long long nzw, int rem) {
                         t_col += wave_count((int)gl < rem);
                         // the <= 8 occupancy bits of this pass's tiles, tested per lane by tile
-                        const uint32_t nzp = pass_bits(nzw, pass);
+                        // (a dense-row tile: every peer's row, whatever its occupancy word says)
+                        const uint32_t nzp = pass_bits(nzw | drm, pass);
                         for (int t0 = 0; t0 < rem; t0 += kInflight) {
                             int open = (a.noskip || !late)
                                            ? 1 : (((want0 & ~acc0) | (want1 & ~acc1)) != 0ull);
@@ -389,8 +457,9 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                         const int rem = min(GRP, end - cb);
                         const int32_t jj = cb + (int32_t)gl;
                         const uint32_t cid = (jj < end) ? (uint32_t)a.col[jj] : 0u;
-                        const unsigned long long nzw = ((int)gl < rem) ? a.nz_cur[(uint64_t)cid * a.ntw + tw] : 0ull;
-                        t_nz += wave_count((int)gl < rem);
+                        const bool ld = (int)gl < rem && nz_needed(idx, tw);
+                        const unsigned long long nzw = ld ? a.nz_cur[(uint64_t)cid * a.ntw + tw] : 0ull;
+                        t_nz += wave_count(ld);
                         gchunk(cid, nzw, rem);
                     }
                 } else {
@@ -447,17 +516,35 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
             // reads every peer row -- the dense-pull byte count)
             int ta = (n0 | n1) != 0ull || (a.noskip && act);
             ta = (int)group_or<8>((uint32_t)ta, lane);
+            // a WF_DW tile's row is written at every node (zeros too): read as a dense row next tick
+            const bool trow = ta || (act && (f0 & WF_DW));
+            // ---- saturation bit of the tile: every live column of it seen, after this tick ----
+            // (want = live & unseen & kept, so want & ~new are the live columns still unseen; a
+            // keep-masked word's dropped columns are unseen too: never saturated on a keep tick)
+            // The bit is updated in place in the node's LDS sat word, which the occupancy word's
+            // last item writes back whole.
+            if (sat_on) {
+                int un = ((want0 & ~n0) | (want1 & ~n1)) != 0ull || ((f0 | f1) & WF_KEEP) != 0u;
+                un = (int)group_or<8>((uint32_t)un, lane);
+                if (act && (wl & 7u) == 0u) {
+                    unsigned long long* sw = s_satw + idx * 2u + (tw - tw_base);
+                    if (un)
+                        atomicAnd(sw, ~tbit);
+                    else
+                        atomicOr(sw, tbit);
+                }
+            }
             // ---- state, counters (one lane per word pair) ----
             const bool own = act && el == 0;
             const bool swr = own && (dead ? ((f0 | f1) & WF_CLEAR) != 0u
                                           : ((n0 | n1) != 0ull || ((f0 | f1) & WF_CLEAR) != 0u));
-            t_fwr += wave_count(own && ta);
+            t_fwr += wave_count(own && trow);
             t_srd += wave_count(own && !dead && !s2c_gated);
             t_swr += wave_count(swr);
             if (own) {
                 uint64_t* sp = a.seen + (uint64_t)v * stride + w;
                 uint64_t* fp = a.Fnext + (uint64_t)v * stride + w;
-                if (ta) store_row16<NT>(fp, n0, n1);
+                if (trow) store_row16<NT>(fp, n0, n1);
                 if (swr) {
                     if (dead && !((f0 & f1) & WF_CLEAR))
                         sp[(f0 & WF_CLEAR) ? 0 : 1] = 0ull;
@@ -486,6 +573,7 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                             a.nz_next[(uint64_t)v * a.ntw + tw] = nzacc;
                         else if (nzacc)
                             atomicOr(&a.nz_next[(uint64_t)v * a.ntw + tw], nzacc);
+                        if (sat_on) a.sat[(uint64_t)v * a.ntw + tw] = s_satw[idx * 2u + (tw - tw_base)];
                     }
                     nzacc = 0ull;
                 }
@@ -520,10 +608,10 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
         if (lane_id == 0 && snap_local) atomicAdd(a.snap, snap_local);
     }
     if (a.acct && lane_id == 0) {
-        const uint32_t tv[6] = {t_pe, t_col, t_srd, t_swr, t_fwr, t_nz};
-        const int slot_of[6] = {0, 1, 2, 3, 4, 7};
+        const uint32_t tv[7] = {t_pe, t_col, t_srd, t_swr, t_fwr, t_nz, t_sk};
+        const int slot_of[7] = {0, 1, 2, 3, 4, 7, 16};
 #pragma unroll
-        for (int q = 0; q < 6; q++)
+        for (int q = 0; q < 7; q++)
             if (tv[q]) acct_add(a.acct, (uint32_t)slot_of[q], (unsigned long long)tv[q]);
     }
     __syncthreads();

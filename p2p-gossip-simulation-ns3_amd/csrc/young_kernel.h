@@ -30,11 +30,24 @@
 // young set.  64 VGPRs (round 3: lane values recomputed per node, explicit-lane shuffles) and ~5
 // KiB of LDS per wave, so that 6-8 waves per SIMD hide the round trips (an explicitly pipelined
 // variant measured no faster: the loop-carried registers forced vmcnt(0) waits, profiles/r02/).
-// Option young_own replaces the seen-word dedup by the node's own frontier of ticks t-1 and t-2
-// (below); measured slower, off by default.
-// Fresh tiles' seen words are cleared here (row by row), and the young words'
-// liveness is reported as all-ones (a young tile is alive by definition; it retires after it
-// leaves the young set, through k_pull's exact liveness).
+// The young words' liveness is reported as all-ones (a young tile is alive by definition; it
+// retires after it leaves the young set, through k_pull's exact liveness).
+//
+// Seen lists (round 4).  A node's processedShares bits in its young tiles are few (C4: ~53 of the
+// ~36k shares of the young tiles, hops <= 4), yet in the dense seen rows every one of them cost an
+// 8-B read and an 8-B write a few per 128-B line (1.3x the bytes), and every fresh tile a 128-B
+// clear per node (8 GB per C4 shard-tick).  So each node keeps them as a LIST of 256 B (header +
+// 127 u16 entries (yid << 10) | (word << 6) | bit, yid = the tile's young id, stable while the tile
+// is young), read with the first batch of peer slots (no dependent seen round trip), applied to
+// the accumulator as AND-NOT, and rewritten in whole lines.  An id group's bits enter the list all
+// together (any seen bit of a group blocks the group, group_fix: holding all of them is the same
+// test).  A tile leaving the young set gets its dense seen rows MATERIALISED (list entries | this
+// tick's new bits, whole 128-B lines: the stale rows of the tile's previous life are overwritten,
+// so fresh tiles need no clear).  A list that would exceed kListCap entries (or k_births' append)
+// OVERFLOWS: the node's dense seen rows of its young tiles are materialised and used from then on
+// (dense words read and written as before, fresh tiles cleared at that node).
+// Header: (kept << 7) | total; entries [1, kept] are the kept entries of earlier ticks, (kept,
+// total] this tick's arrivals (and births): k_births tests an id group against the former only.
 #pragma once
 
 constexpr uint32_t kSlotU16 = 128;           // 256 B per node per frontier buffer
@@ -43,14 +56,22 @@ constexpr uint32_t kSlotTomb = 0xffffu;      // entry: removed (id-group birth b
 constexpr uint32_t kYoungMax = 48;           // tiles per launch
 constexpr uint32_t kYoungWriteMax = 40;      // write-sparse tiles per tick (w_idx < 40 <= 62)
 constexpr int kYoungQ = 3;  // slot-line loads per batch: 24 peers (C4: P(deg > 24) ~ 2 %)
-enum : uint32_t { YT_READ = 1u, YT_WRITE = 2u };
+constexpr uint32_t kListU16 = 128;           // seen list: 256 B per node (header + 127 entries)
+constexpr uint32_t kListOverflow = 0xffffu;  // header: the dense seen rows of the young tiles are valid
+constexpr uint32_t kListReserve = 8;         // entries left for k_births' appends after k_pull_young
+constexpr uint32_t kListCap = kListU16 - 1u - kListReserve;  // k_pull_young overflows a list beyond this
+constexpr uint32_t kYidNone = 0xffu;
+__host__ __device__ constexpr uint32_t list_header(uint32_t kept, uint32_t total) { return (kept << 7) | total; }
+// YT_DW (a leaving tile): write every node's dense row, zeros too -- k_pull reads the tile next
+// tick as dense rows, without occupancy words (pull_kernel.h)
+enum : uint32_t { YT_READ = 1u, YT_WRITE = 2u, YT_DW = 4u };
 
 struct YoungTile {
     uint32_t tile;
     uint8_t flags;  // YT_READ: F_cur holds this tile in slots; YT_WRITE: F_next goes to slots
     uint8_t r_idx;  // w_idx of this tile in F_cur's entries (YT_READ)
     uint8_t w_idx;  // index written into F_next's entries (YT_WRITE)
-    uint8_t pad;
+    uint8_t yid;    // young id: the tile's index in the seen lists' entries while it is young
 };
 
 // yt order (host): [0, nr) the read-sparse tiles BY THEIR INDEX IN F_cur's ENTRIES (so an entry
@@ -90,23 +111,34 @@ struct YoungArgs {
     uint8_t* hint_next;
     const int32_t* rev;
     uint32_t stamp_cur, stamp_next;
-    // Own-frontier dedup (option young_own): a node's processed bits among its incoming ones are
-    // exactly its own frontier bits of the last two ticks (see k_pull_young), read from its own
-    // slots -- F_{t-1} in slot_cur, F_{t-2} in slot_next before this tick overwrites it -- in the
-    // same round trip as the peers' slots.  map2[w] = the read position of the tile whose t-2
-    // write index was w (0xff: none); n2 = entries of t-2's write list (0: slot_next is stale).
-    const uint8_t* map2;
-    uint32_t own, n2;
     uint32_t slot_nt;  // option young_nt: non-temporal slot-line loads (C4 shard, young alone 21.1 -> 19.0 ms)
+    uint16_t* list;        // n x kListU16 seen lists
+    const uint8_t* ymap;   // [64] young id -> position in yt (0xff: none)
+    uint32_t list_cap;     // entries a list may keep (kListCap; option young_list_cap for tests)
 };
 
 constexpr uint32_t kYoungSpare = 32;  // spare accumulator words per wave (tombstones land here)
 
 __host__ __device__ constexpr size_t young_lds_bytes(uint32_t ny, uint32_t nr) {
     // 4 waves x (accumulator 8 B per read word + spares, touched list 2 B per read word, a slot
-    // staging buffer), tiles, read-word flags, leaving positions
+    // and a seen-list staging buffer), tiles, read-word flags, leaving positions, young ids
     return 4u * ((size_t)nr * 16u + kYoungSpare) * 8u + 4u * (size_t)nr * 16u * 2u + 4u * kSlotU16 * 2u +
-           (size_t)ny * sizeof(YoungTile) + (size_t)nr * 16u + 64u + 64u;
+           4u * kListU16 * 2u + (size_t)ny * sizeof(YoungTile) + (size_t)nr * 16u + 64u + 64u;
+}
+
+// x with every id group it touches made whole (gm / gs: the word's group bits and group starts;
+// groups are contiguous runs, group_fix's layout)
+__device__ __forceinline__ uint64_t group_expand(uint64_t x, uint64_t gm, uint64_t gs) {
+    uint64_t rem = gm, out = x;
+    while (rem & x) {
+        const int s = __ffsll((long long)rem) - 1;
+        const uint64_t above = gs & ~((2ull << s) - 1ull);
+        const uint64_t upto = above ? ((above & (~above + 1ull)) - 1ull) : ~0ull;
+        const uint64_t grp = rem & upto;
+        if (x & grp) out |= grp;
+        rem &= ~grp;
+    }
+    return out;
 }
 
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane) {
@@ -129,9 +161,8 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m, uint32_t l
     return (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-// WAVES: waves per SIMD the register allocation must allow (young_waves option; 4 = no spills)
-template <int WAVES>
-__global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
+// 256-thread blocks; the register budget of 4 waves per SIMD (5 and 6 spilled: round 3)
+__global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
     extern __shared__ unsigned long long smem[];
     const uint32_t nrw = a.nr * 16u;  // accumulated words
     const uint32_t accw = nrw + kYoungSpare;
@@ -139,13 +170,15 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
     unsigned long long* s_acc = smem + wv * accw;
     uint16_t* s_list = reinterpret_cast<uint16_t*>(smem + 4u * accw) + wv * nrw;
     uint16_t* s_out = reinterpret_cast<uint16_t*>(smem + 4u * accw) + 4u * nrw + wv * kSlotU16;  // 16-B aligned
-    YoungTile* s_yt = reinterpret_cast<YoungTile*>(reinterpret_cast<uint16_t*>(smem + 4u * accw) + 4u * nrw + 4u * kSlotU16);
+    uint16_t* s_lst = reinterpret_cast<uint16_t*>(smem + 4u * accw) + 4u * nrw + 4u * kSlotU16 + wv * kListU16;
+    YoungTile* s_yt = reinterpret_cast<YoungTile*>(reinterpret_cast<uint16_t*>(smem + 4u * accw) + 4u * nrw +
+                                                   4u * kSlotU16 + 4u * kListU16);
     uint8_t* s_wf = reinterpret_cast<uint8_t*>(s_yt + a.ny);
     uint8_t* s_lv = s_wf + nrw;
-    uint8_t* s_map2 = s_lv + 64;
+    uint8_t* s_ymap = s_lv + 64;
     for (uint32_t i = threadIdx.x; i < a.ny; i += 256) s_yt[i] = a.yt[i];
     if (threadIdx.x < a.nt) s_lv[threadIdx.x] = a.lv[threadIdx.x];
-    if (threadIdx.x < 64u) s_map2[threadIdx.x] = threadIdx.x < a.n2 ? a.map2[threadIdx.x] : (uint8_t)0xffu;
+    if (threadIdx.x < 64u) s_ymap[threadIdx.x] = a.ymap[threadIdx.x];
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nrw; i += 256) s_wf[i] = a.wflags[s_yt[i >> 4].tile * 16u + (i & 15u)];
     for (uint32_t i = lane_id; i < accw; i += 64) s_acc[i] = 0ull;
@@ -157,8 +190,10 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     const uint64_t stride = a.stride;
     unsigned long long snap_local = 0ull;
-    // traffic (wave-uniform): slot lines, peer ids, dense fallback rows, seen r/w, row/slot writes
+    // traffic (wave-uniform): slot lines, peer ids, dense fallback rows, seen r/w, row/slot writes,
+    // unhinted second lines, seen-list lines read / written, seen rows materialised / cleared
     uint32_t t_sl = 0, t_col = 0, t_fb = 0, t_srd = 0, t_swr = 0, t_rw = 0, t_slw = 0, t_miss = 0;
+    uint32_t t_lr = 0, t_lw = 0, t_mat = 0;
 
     for (uint64_t c0 = a.v0 + wave * 64u; c0 < a.n; c0 += nwaves * 64u) {
         const uint32_t lane = opaque(lane_id);
@@ -280,14 +315,12 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
             };
             const int32_t np0 = min(64, end - beg);
             t_col += (uint32_t)max(0, end - beg);
-            if (a.own) t_sl += a.n2 ? 4u : 2u;  // the own slots' lines
             unsigned long long ovf = 0ull;
             issue(cid_cur, 0);
-            // own slots (lanes 0-15: F_{t-1}'s two lines, 16-31: F_{t-2}'s), with the first batch
-            ulonglong2 qo = make_ulonglong2(~0ull, ~0ull);
-            if (a.own && (lane < 16u || (lane < 32u && a.n2)))
-                qo = *reinterpret_cast<const ulonglong2*>((lane < 16u ? a.slot_cur : a.slot_next) + v * kSlotU16 +
-                                                          (lane & 15u) * 8u);
+            // own seen list (lanes 0-15: its two lines), with the first batch
+            ulonglong2 ql = make_ulonglong2(~0ull, ~0ull);
+            if (lane < 16u) ql = *reinterpret_cast<const ulonglong2*>(a.list + v * kListU16 + lane * 8u);
+            t_lr += 2u;
             uint32_t h_next = 0u;
             const uint32_t cid_next = load_ids(jn + 1u, h_next);  // the next node's peers
             consume(cid_cur, 0, np0, ovf);
@@ -310,38 +343,35 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                 }
                 fallback(cid, ovf2);
             }
-            // ---- own-frontier dedup: clear the incoming bits the node already holds ----
-            // The floods are breadth-first searches advancing one hop per tick, so a node v adjacent
-            // to a peer u that first saw share s at tick t-1 first saw s at t-2, t-1 or t (v's
-            // sends reach u one tick later, and u's reach v).  So among v's incoming bits at tick t
-            // the processed ones (p2pnode.cc:189) are exactly v's frontier bits of ticks t-1 and
-            // t-2: v's own slots, already in registers -- no dependent load of v's seen words.  Id
-            // group words (several sources for one id, group_fix) and nodes whose own slot
-            // overflowed (their frontier is in dense rows) still read seen (need_sv below).
-            bool own_ovf = !a.own;
-            if (a.own) {
-                const uint32_t h1 = lane_read((uint32_t)(qo.x & 0xffffull), 0u);
-                const uint32_t h2 = lane_read((uint32_t)(qo.x & 0xffffull), 16u);
-                own_ovf = h1 == kSlotOverflow || (a.n2 && h2 == kSlotOverflow);
-                if (!own_ovf) {
-                    __builtin_amdgcn_wave_barrier();
-                    const uint32_t piece = lane & 15u;  // 16-B piece: 0-7 first line, 8-15 second
-                    const bool prev2 = lane >= 16u;
-                    const bool valid = lane < 32u && (!prev2 || a.n2) && (piece < 8u || (prev2 ? h2 : h1) > 63u);
-                    if (valid) {
+            // ---- seen list: clear the incoming bits the node already holds (p2pnode.cc:189) ----
+            const uint32_t lhdr = lane_read((uint32_t)(ql.x & 0xffffull), 0u);
+            const bool lovf = lhdr == kListOverflow;  // (uniform) dense seen rows instead
+            const uint32_t ltot = lovf ? 0u : (lhdr & 127u);
+            // entry j of this lane's piece: kept into the new list (its tile stays young)
+            uint32_t keepm = 0u;
+            reinterpret_cast<uint32_t*>(s_lst)[lane] = 0xffffffffu;  // tombstones
+            __builtin_amdgcn_wave_barrier();
+            if (!lovf && lane < 16u) {
 #pragma unroll
-                        for (int j = 0; j < 8; j++) {
-                            const uint32_t e = (j == 0 && piece == 0u) ? kSlotTomb : slot_entry(qo, j);
-                            if (e == kSlotTomb) continue;
-                            uint32_t w = e >> 6;  // F_{t-1}: read position r * 16 + word
-                            if (prev2) {          // F_{t-2}: t-2's write index -> read position
-                                const uint32_t r = s_map2[e >> 10];
-                                w = r == 0xffu ? spare : r * 16u + ((e >> 6) & 15u);
-                            }
-                            atomicAnd(reinterpret_cast<uint32_t*>(s_acc + min(w, spare)) + ((e >> 5) & 1u), ~(1u << (e & 31u)));
-                        }
-                    }
+                for (int j = 0; j < 8; j++) {
+                    const uint32_t idx = lane * 8u + (uint32_t)j;
+                    const uint32_t e = slot_entry(ql, j);
+                    if (idx == 0u || idx > ltot || e == kSlotTomb) continue;
+                    const uint32_t qp = s_ymap[e >> 10];
+                    if (qp >= a.ny) continue;  // (a tile no longer young: dropped)
+                    if (qp < a.nr)
+                        atomicAnd(reinterpret_cast<uint32_t*>(s_acc + qp * 16u + ((e >> 6) & 15u)) + ((e >> 5) & 1u),
+                                  ~(1u << (e & 31u)));
+                    if (s_yt[qp].flags & YT_WRITE) keepm |= 1u << j;
                 }
+            }
+            // kept entries -> s_lst[1, kept]
+            uint32_t kept = 0;
+            {
+                const uint32_t c = (uint32_t)__builtin_popcount(keepm);
+                uint32_t pos = 1u + wave_excl_scan(c, lane);
+                kept = wave_sum32(c);
+                for (uint32_t m = keepm; m; m &= m - 1u) s_lst[pos++] = (uint16_t)slot_entry(ql, __builtin_ctz(m));
             }
             __builtin_amdgcn_wave_barrier();
             // ---- touched words -> list ----
@@ -354,18 +384,18 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                 ntouch += (uint32_t)__popcll(m);
             }
             __builtin_amdgcn_wave_barrier();
-            // ---- dedup against the own seen words (the first 4 x 64 loads issued together) ----
-            // (own-frontier dedup: only for id-group words, or every word of an overflowed node)
+            // ---- dedup (an overflowed list: against the dense seen words, the first 4 x 64 loads
+            //      issued together); new seen entries of the tiles staying young -> s_lst ----
             uint32_t cnt = 0, cnt_sp = 0;
+            uint32_t total = 1u + kept;  // next free entry of s_lst
             uint64_t svq[4];
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const uint32_t t = (uint32_t)r * 64u + lane;
                 svq[r] = 0ull;
-                if (t < ntouch) {
+                if (lovf && t < ntouch) {
                     const uint32_t i = s_list[t];
-                    if (own_ovf || (s_wf[i] & WF_GROUP))
-                        svq[r] = a.seen[v * stride + s_yt[i >> 4].tile * 16u + (i & 15u)];
+                    svq[r] = a.seen[v * stride + s_yt[i >> 4].tile * 16u + (i & 15u)];
                 }
             }
             for (uint32_t t0 = 0; t0 < ntouch; t0 += 64) {
@@ -374,42 +404,51 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                 const uint32_t i = valid ? s_list[t] : 0u;
                 const YoungTile yt = s_yt[i >> 4];
                 const uint32_t w = yt.tile * 16u + (i & 15u);
-                uint64_t x = 0ull;
-                bool need_sv = false;
+                uint64_t x = 0ull, xe = 0ull;
                 if (valid) {
                     const uint32_t f = s_wf[i];
-                    need_sv = own_ovf || (f & WF_GROUP);
                     uint64_t* sp = a.seen + v * stride + w;
                     const uint32_t r = t0 >> 6;
-                    const uint64_t sv = !need_sv ? 0ull : r == 0 ? svq[0] : r == 1 ? svq[1] : r == 2 ? svq[2] : r == 3 ? svq[3] : *sp;
+                    const uint64_t sv = !lovf ? 0ull : r == 0 ? svq[0] : r == 1 ? svq[1] : r == 2 ? svq[2] : r == 3 ? svq[3] : *sp;
                     const uint64_t keep = (f & WF_KEEP) ? a.ctl[w].keep : ~0ull;
                     x = s_acc[i] & ~sv & keep;
+                    // (a list holds every bit of a seen group: the accumulator has none of them)
                     if (f & WF_GROUP) x = group_fix(x, sv, a.ctl[w].gmask, a.ctl[w].gstart);
-                    if (x) {
-                        if (need_sv)
-                            *sp = sv | x;
-                        else  // (no-return atomic: the word's old value is not needed)
-                            atomicOr(reinterpret_cast<unsigned long long*>(sp), (unsigned long long)x);
-                    }
+                    if (lovf && x) *sp = sv | x;
                     if (a.snap && (f & WF_SNAP)) snap_local += (unsigned long long)__popcll(x & a.ctl[w].snap);
                     s_acc[i] = x;  // the node's new bits, for the outputs below
+                    xe = (f & WF_GROUP) ? group_expand(x, a.ctl[w].gmask, a.ctl[w].gstart) : x;
                 }
                 cnt += (uint32_t)__popcll(x);
                 if (yt.flags & YT_WRITE) cnt_sp += (uint32_t)__popcll(x);
-                t_srd += wave_count(need_sv);
-                t_swr += wave_count(x != 0ull);
+                t_srd += wave_count(lovf && valid);
+                t_swr += wave_count(lovf && x != 0ull);
+                // the list's new entries (tiles staying young), positions by a wave prefix sum
+                uint64_t xl = (!lovf && (yt.flags & YT_WRITE)) ? xe : 0ull;
+                const uint32_t c = (uint32_t)__popcll(xl);
+                uint32_t pos = total + wave_excl_scan(c, lane);
+                total += wave_sum32(c);
+                while (xl) {
+                    const uint32_t bb = (uint32_t)__builtin_ctzll(xl);
+                    xl &= xl - 1ull;
+                    if (pos < kListU16)
+                        s_lst[pos] = (uint16_t)(((uint32_t)yt.yid << 10) | ((i & 15u) << 6) | bb);
+                    pos++;
+                }
             }
+            const uint32_t lcount = total - 1u;
+            const bool lspill = !lovf && lcount > a.list_cap;  // (uniform) the list overflows now
             __builtin_amdgcn_wave_barrier();
             cid_cur = with_hint(cid_next, h_next);  // (arrived long ago: the wait is before the stores)
             // ---- output: slot entries, or dense rows (overflowed / leaving the young set) ----
-            const uint32_t total = wave_sum32(cnt_sp);
-            const bool overflow = total > a.cap;
+            const uint32_t slot_total = wave_sum32(cnt_sp);
+            const bool overflow = slot_total > a.cap;
             uint16_t* out = a.slot_next + v * kSlotU16;
             // the slot is staged in LDS and written as whole lines (no partial-line writes); every
             // unused entry is a tombstone (readers scatter whole lines)
             reinterpret_cast<uint32_t*>(s_out)[lane] = 0xffffffffu;
             __builtin_amdgcn_wave_barrier();
-            if (!overflow && total) {
+            if (!overflow && slot_total) {
                 uint32_t base = 1;
                 for (uint32_t t0 = 0; t0 < ntouch; t0 += 64) {
                     const uint32_t t = t0 + lane;
@@ -426,10 +465,10 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                     base += wave_sum32(c);
                 }
             }
-            if (lane == 0) s_out[0] = (uint16_t)(overflow ? kSlotOverflow : total);
+            if (lane == 0) s_out[0] = (uint16_t)(overflow ? kSlotOverflow : slot_total);
             __builtin_amdgcn_wave_barrier();
             {
-                const uint32_t lines = (!overflow && total > 63u) ? 2u : 1u;
+                const uint32_t lines = (!overflow && slot_total > 63u) ? 2u : 1u;
                 if (lane < 8u * lines)
                     *reinterpret_cast<ulonglong2*>(out + lane * 8u) = *reinterpret_cast<const ulonglong2*>(s_out + lane * 8u);
                 t_slw += lines;
@@ -449,13 +488,13 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                 const bool in = qi < ndense;
                 const uint32_t q = !in ? 0u : overflow ? qi : (uint32_t)s_lv[qi];
                 const YoungTile yt = s_yt[q];
-                const bool leaving = in && (yt.flags & (YT_READ | YT_WRITE)) == YT_READ;
+                const bool leaving = in && (yt.flags & (YT_READ | YT_WRITE)) == YT_READ;  // (YT_DW or not)
                 const bool dense_out = leaving || (in && (yt.flags & YT_WRITE));
                 const uint64_t x = (in && q < a.nr) ? s_acc[q * 16u + word] : 0ull;
                 const unsigned long long m = __ballot(in && x != 0ull);
                 const bool tany = ((m >> (lane & ~15u)) & 0xffffull) != 0ull;
                 // overflowed nodes write every write-sparse row (readers check no occupancy)
-                const bool wr = dense_out && (tany || !leaving);
+                const bool wr = dense_out && (tany || !leaving || (yt.flags & YT_DW));
                 if (wr) a.Fnext[v * stride + yt.tile * 16u + word] = x;
                 t_rw += wave_count(wr && word == 0u);
                 if (leaving && tany && word == 0u) {
@@ -469,15 +508,76 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
                 }
             }
             if (nzw) atomicOr(&a.nz_next[v * a.ntw + nz_tw], nzw);
+            __builtin_amdgcn_wave_barrier();
+            // ---- seen rows materialised from the list: the tiles leaving the young set, or (the
+            //      list overflows now) every young position; whole 128-B lines ----
+            if (!lovf) {
+                const uint32_t nm = lspill ? a.ny : a.nt;
+                // (1) the new bits of those tiles with their id groups made whole
+                for (uint32_t q0 = 0; q0 < nm; q0 += 4) {
+                    const uint32_t qi = q0 + (lane >> 4), word = lane & 15u;
+                    const uint32_t q = qi >= nm ? 0xffffffffu : lspill ? qi : (uint32_t)s_lv[qi];
+                    if (q < a.nr) {
+                        const uint32_t i = q * 16u + word;
+                        const uint64_t x = s_acc[i];
+                        if (x && (s_wf[i] & WF_GROUP)) {
+                            const uint32_t w = s_yt[q].tile * 16u + word;
+                            s_acc[i] = group_expand(x, a.ctl[w].gmask, a.ctl[w].gstart);
+                        }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                // (2) the old entries of those tiles
+                if (lane < 16u) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const uint32_t idx = lane * 8u + (uint32_t)j;
+                        const uint32_t e = slot_entry(ql, j);
+                        if (idx == 0u || idx > ltot || e == kSlotTomb) continue;
+                        const uint32_t qp = s_ymap[e >> 10];
+                        if (qp >= a.nr) continue;
+                        const bool leaving = (s_yt[qp].flags & (YT_READ | YT_WRITE)) == YT_READ;
+                        if (lspill || leaving)
+                            atomicOr(reinterpret_cast<uint32_t*>(s_acc + qp * 16u + ((e >> 6) & 15u)) + ((e >> 5) & 1u),
+                                     1u << (e & 31u));
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                // (3) write the rows (fresh positions: zeros), (4) reset their accumulator words
+                for (uint32_t q0 = 0; q0 < nm; q0 += 4) {
+                    const uint32_t qi = q0 + (lane >> 4), word = lane & 15u;
+                    const uint32_t q = qi >= nm ? 0xffffffffu : lspill ? qi : (uint32_t)s_lv[qi];
+                    if (q != 0xffffffffu && s_yt[q].flags) {
+                        const uint64_t x = q < a.nr ? s_acc[q * 16u + word] : 0ull;
+                        a.seen[v * stride + s_yt[q].tile * 16u + word] = x;
+                        if (q < a.nr) s_acc[q * 16u + word] = 0ull;
+                    }
+                    t_mat += wave_count(q != 0xffffffffu && s_yt[q].flags && word == 0u);
+                }
+            }
+            // ---- the new seen list: whole lines; an overflow marks the header ----
+            if (!lovf) {
+                if (lane == 0) s_lst[0] = (uint16_t)(lspill ? kListOverflow : list_header(kept, lcount));
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t lines = (!lspill && lcount > 63u) ? 2u : 1u;
+                if (lane < 8u * lines)
+                    *reinterpret_cast<ulonglong2*>(a.list + v * kListU16 + lane * 8u) =
+                        *reinterpret_cast<const ulonglong2*>(s_lst + lane * 8u);
+                t_lw += lines;
+            }
             // ---- reset the touched accumulator words, counters ----
             for (uint32_t t = lane; t < ntouch; t += 64) s_acc[s_list[t]] = 0ull;
             __builtin_amdgcn_wave_barrier();
-            // fresh write-sparse tiles [nr, ny): clear their seen words (stale from the tiles'
-            // previous use; k_births sets this tick's own-generation bits after this kernel)
-            for (uint32_t q0 = a.nr; q0 < a.ny; q0 += 4) {
-                const uint32_t q = q0 + (lane >> 4);
-                if (q < a.ny) a.seen[v * stride + s_yt[q].tile * 16u + (lane & 15u)] = 0ull;
-            }
+            // fresh write-sparse tiles [nr, ny) of a node whose list overflowed (earlier): clear
+            // their dense seen words (stale from the tiles' previous use; k_births sets this tick's
+            // own-generation bits after this kernel).  A list node's fresh rows are written whole
+            // when they leave the young set.
+            if (lovf)
+                for (uint32_t q0 = a.nr; q0 < a.ny; q0 += 4) {
+                    const uint32_t qq = q0 + (lane >> 4);
+                    if (qq < a.ny) a.seen[v * stride + s_yt[qq].tile * 16u + (lane & 15u)] = 0ull;
+                    t_mat += wave_count(qq < a.ny && (lane & 15u) == 0u);
+                }
             const uint32_t c = wave_sum32(cnt);
             if (lane == 0 && c) {  // no-return atomics: nothing waits on them
                 atomicAdd(&a.recv[v], c);
@@ -490,9 +590,10 @@ __global__ __launch_bounds__(256, WAVES) void k_pull_young(YoungArgs a) {
         if (lane_id == 0 && snap_local) atomicAdd(a.snap, snap_local);
     }
     if (a.acct && lane_id == 0) {
-        const uint32_t tv[8] = {t_sl, t_col, t_fb, t_srd, t_swr, t_rw, t_slw, t_miss};
+        const uint32_t tv[11] = {t_sl, t_col, t_fb, t_srd, t_swr, t_rw, t_slw, t_miss, t_lr, t_lw, t_mat};
+        const uint32_t slot_of[11] = {8, 9, 10, 11, 12, 13, 14, 15, 17, 18, 19};
 #pragma unroll
-        for (int q = 0; q < 8; q++)
-            if (tv[q]) acct_add(a.acct, 8 + q, (unsigned long long)tv[q]);
+        for (int q = 0; q < 11; q++)
+            if (tv[q]) acct_add(a.acct, slot_of[q], (unsigned long long)tv[q]);
     }
 }

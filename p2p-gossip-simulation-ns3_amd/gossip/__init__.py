@@ -110,6 +110,9 @@ class gossip_counters(C.Structure):
         ("pull_phase_ms", C.c_double), ("young_line2_misses", C.c_uint64),
         ("pull_late_age", C.c_uint32), ("pull_tiles", C.c_uint32),
         ("young_fresh_lines", C.c_uint64),
+        ("pull_lpw", C.c_uint32), ("pull_dense_tiles", C.c_uint32),
+        ("pull_sat_skips", C.c_uint64), ("pull_sat", C.c_uint32), ("pad0", C.c_uint32),
+        ("window_early_retires", C.c_uint64), ("young_list_lines", C.c_uint64),
     ]
 
 
@@ -425,6 +428,10 @@ class Engine:
     def connect_rccl(self, unique_id: bytes):
         _check(load_library().gossip_engine_connect_rccl(self._h, unique_id, len(unique_id)),
                "rccl connect")
+
+    def abort(self):
+        """gossip_engine_abort: tear down the communicator (if any); later steps fail (E_STATE)."""
+        _check(load_library().gossip_engine_abort(self._h), "abort")
 
     # ---- host-staged row exchange (gossip.h): one message per rank and tick, or per row chunk --
     def tick_begin(self) -> bool:

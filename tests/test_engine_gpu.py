@@ -14,8 +14,10 @@ pytestmark = pytest.mark.gpu
 STATS = ("gen", "recv", "fwd", "sent", "processed", "peers", "sockets")
 
 
-def _engine_for(gossip, topo, events, latency_ns, t_cut, snapshots=(), flags=0, **kw):
+def _engine_for(gossip, topo, events, latency_ns, t_cut, snapshots=(), flags=0, options=(), **kw):
     eng = gossip.Engine(topo.num_nodes, latency_ns, T0, t_cut, flags=flags, **kw)
+    for k, v in options:
+        eng.set_option(k, v)
     eng.set_topology(topo)
     for s in snapshots:
         eng.add_snapshot(s)
@@ -80,13 +82,13 @@ def test_report_text_matches_oracle(gossip, oracle):
 KERNELS = {"auto": 0, "wide": 8, "generic": 16}
 
 
-def _trace_parity(gossip, oracle, n, p, seed, sim_time, lat_ms, kind=None, id_mask=0, kflags=0):
+def _trace_parity(gossip, oracle, n, p, seed, sim_time, lat_ms, kind=None, id_mask=0, kflags=0, options=()):
     kind = gossip.TOPO_EXACT if kind is None else kind
     topo = gossip.Topology.gnp(n, p, seed, kind)
     lat = gossip.milliseconds_to_ns(lat_ms)
     t_cut = gossip.seconds_to_ns(sim_time - 0.1)
     ev = gossip.make_schedule(n, seed + 1, T0, t_cut, id_mask=id_mask)
-    eng = _engine_for(gossip, topo, ev, lat, t_cut, flags=gossip.F_TRACE | kflags)
+    eng = _engine_for(gossip, topo, ev, lat, t_cut, flags=gossip.F_TRACE | kflags, options=options)
     st = eng.stats()
     a, b = topo.links()
     r = oracle.run_replay(n, lat, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=True)
@@ -121,6 +123,30 @@ def test_trace_parity_collisions(gossip, oracle, kern):
 @pytest.mark.parametrize("kern", list(KERNELS))
 def test_trace_parity_odd_latency(gossip, oracle, kern):
     _trace_parity(gossip, oracle, 300, 0.02, 24, 10.37, 2.3, kflags=KERNELS[kern])
+
+
+# Saturation bits and dense-row tiles (pull_kernel.h) against the oracle's counters and traces:
+# forced dense rows on every listed tile (every k_pull row written, read without occupancy words),
+# saturation bits off / on, where id groups (collisions: births landing in old tiles, whose sat
+# bits must not be trusted), odd latencies (the in-tick cut: keep masks) and tile reuse happen.
+SAT_DR = {"dr_forced": (("dense_rows", 1),), "dr_forced_nosat": (("dense_rows", 1), ("pull_sat", 0)),
+          "sat_only": (("dense_rows", 0),), "both_off": (("dense_rows", 0), ("pull_sat", 0))}
+
+
+@pytest.mark.parametrize("opts", list(SAT_DR))
+def test_sat_dense_rows_collisions(gossip, oracle, opts):
+    _trace_parity(gossip, oracle, 400, 0.01, 23, 15.0, 5.0, id_mask=0x3FF, options=SAT_DR[opts])
+
+
+@pytest.mark.parametrize("opts", list(SAT_DR))
+def test_sat_dense_rows_odd_latency_wide(gossip, oracle, opts):
+    _trace_parity(gossip, oracle, 3000, 8.0 / 2999, 27, 6.37, 2.3, kind=gossip.TOPO_SKIP,
+                  kflags=gossip.F_TILE_PER_TICK, options=SAT_DR[opts])
+
+
+@pytest.mark.parametrize("opts", list(SAT_DR))
+def test_sat_dense_rows_sparse_4096(gossip, oracle, opts):
+    _trace_parity(gossip, oracle, 4096, 16.0 / 4095, 21, 6.0, 5.0, options=SAT_DR[opts])
 
 
 @pytest.mark.parametrize("n,p,id_mask,sim", [(512, 0.3, 0, 8.0), (300, 0.05, 0xFFF, 30.0),
@@ -158,20 +184,33 @@ def test_work_skipping_changes_nothing(gossip, kern):
 
 
 def test_wide_window_kernels_agree(gossip, oracle):
-    # A window far wider than 64 words (a fresh tile every tick): the default (k_pull_wide at
-    # this width) and the lane-shuffle kernel must match the oracle bit for bit.
+    # A window far wider than 64 words (a fresh tile every tick): every pull kernel, and the
+    # production instantiation k_pull<32, 1, true> (non-temporal rows) with and without young-tile
+    # slots, must match the oracle bit for bit.
     n = 3000
     topo = gossip.Topology.gnp(n, 6.0 / (n - 1), 43, gossip.TOPO_SKIP)
     t_cut = gossip.seconds_to_ns(5.7)
     ev = gossip.make_schedule(n, 7, T0, t_cut)
     a, b = topo.links()
     r = oracle.run_replay(n, L, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
-    for kern in KERNELS.values():
-        eng = _engine_for(gossip, topo, ev, L, t_cut, flags=kern | gossip.F_TILE_PER_TICK)
-        st = eng.stats()
-        assert eng.counters().words_hw > 64
+    runs = [(kern, {}) for kern in KERNELS.values()]
+    runs += [(0, {"pull_nt": 1}), (0, {"pull_nt": 1, "young": 1, "young_nt": 1, "pull_grid": 16384}),
+             (0, {"pull_nt": 1, "dense_rows": 1}), (0, {"pull_nt": 1, "pull_sat": 0, "dense_rows": 0})]
+    for kern, opts in runs:
+        eng = gossip.Engine(n, L, T0, t_cut, flags=kern | gossip.F_TILE_PER_TICK)
+        for k, v in opts.items():
+            eng.set_option(k, v)
+        eng.set_topology(topo)
+        eng.set_schedule(ev)
+        eng.run()
+        eng.sync()
+        st, c = eng.stats(), eng.counters()
+        eng.close()
+        assert c.words_hw > 64
+        if opts.get("pull_nt"):
+            assert c.pull_nt == 1 and c.pull_lpw == 32, opts  # k_pull<32, 1, true>
         for k in STATS:
-            assert np.array_equal(getattr(st, k), getattr(r, k)), (kern, k)
+            assert np.array_equal(getattr(st, k), getattr(r, k)), (kern, opts, k)
 
 
 def test_tile_list_options_agree(gossip, oracle):
@@ -186,7 +225,10 @@ def test_tile_list_options_agree(gossip, oracle):
     r = oracle.run_replay(n, L, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=True)
     tn, ti, tt, th, tv = r.trace
     ok = np.lexsort((ti, tn))
-    for opts in ({}, {"pull_tile_order": 0}, {"pull_tiles": 0}):
+    prod = {"pull_nt": 1, "pull_grid": 16384, "pull_tile_order": 1}  # the C4 bench's k_pull<32,1,true>
+    for opts in ({}, {"pull_tile_order": 0}, {"pull_tiles": 0}, prod,
+                 dict(prod, young=1, young_nt=1), dict(prod, young=1, young_nt=1, dense_rows=1),
+                 dict(prod, dense_rows=1), dict(prod, dense_rows=1, pull_sat=0), {"pull_sat": 0, "dense_rows": 0}):
         eng = gossip.Engine(n, L, T0, t_cut, flags=gossip.F_TILE_PER_TICK | gossip.F_TRACE | gossip.F_GENERIC_PULL)
         for k, v in opts.items():
             eng.set_option(k, v)
@@ -196,6 +238,10 @@ def test_tile_list_options_agree(gossip, oracle):
         eng.sync()
         st, c = eng.stats(), eng.counters()
         assert c.words_hw > 64 and (c.pull_tiles == 0 or opts.get("pull_tiles") != 0), opts
+        if opts.get("pull_nt"):
+            assert c.pull_nt == 1 and c.pull_lpw == 32 and c.pull_grid == 12, opts  # (3,000 nodes: 12 blocks)
+        if opts.get("young"):
+            assert c.young_launches > 0, opts
         for k in STATS:
             assert np.array_equal(getattr(st, k), getattr(r, k)), (opts, k)
         node, sid, tick, hop, via = eng.trace()
@@ -214,6 +260,27 @@ def test_window_growth_is_transparent(gossip, oracle):
     eng = _engine_for(gossip, topo, ev, L, t_cut, max_words=16)
     st = eng.stats()
     assert eng.counters().words_cap > 16
+    a, b = topo.links()
+    r = oracle.run_replay(n, L, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
+    for k in STATS:
+        assert np.array_equal(getattr(st, k), getattr(r, k)), k
+
+
+def test_early_retire_near_capacity(gossip, oracle):
+    # A window sized to the run's own peak: near its capacity the allocator first retires tiles from
+    # the last tick's liveness (one tick earlier than the regular two-tick lag) instead of widening
+    # the window -- results unchanged, no growth
+    n = 3000
+    topo = gossip.Topology.gnp(n, 8.0 / (n - 1), 42, gossip.TOPO_SKIP)
+    t_cut = gossip.seconds_to_ns(7.0)
+    ev = gossip.make_schedule(n, 6, T0, t_cut)
+    free = _engine_for(gossip, topo, ev, L, t_cut, flags=gossip.F_TILE_PER_TICK)
+    peak = free.counters().words_hw
+    free.close()
+    eng = _engine_for(gossip, topo, ev, L, t_cut, flags=gossip.F_TILE_PER_TICK, max_words=peak)
+    st, c = eng.stats(), eng.counters()
+    eng.close()
+    assert c.window_early_retires > 0 and c.words_cap == peak and c.words_hw <= peak
     a, b = topo.links()
     r = oracle.run_replay(n, L, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
     for k in STATS:

@@ -101,6 +101,34 @@ def test_rccl_one_rank_matches_single_engine(gossip, mode, p):
     ref.close()
 
 
+def test_abort_refuses_further_steps(gossip):
+    # gossip_engine_abort (a failing rank tears its partition down): the communicator is freed, so
+    # every later step of the engine -- and every collective its thread would still issue -- must
+    # fail with E_STATE instead of touching it
+    n = 1000
+    topo, t_cut, ev = _inputs(gossip, n, 0.01, 41, 7.0)
+    e = _engine(gossip, n, t_cut, topo, ev, gossip.MODE_CSR, 0, part=(0, 1))
+    e.connect_rccl(gossip.rccl_unique_id())
+    e.run(e.first_tick + 50)
+    e.sync()
+    e.abort()
+    e.abort()  # idempotent
+    with pytest.raises(gossip.GossipError, match="aborted") as ex:
+        e.run()
+    assert ex.value.code == gossip.E_STATE
+    e.close()
+    # without a communicator: host-staged stepping and the lockstep backend refuse it too
+    topo2, t_cut2, ev2 = _inputs(gossip, 1100, 0.02, 51, 6.0)
+    ranks = [_engine(gossip, 1100, t_cut2, topo2, ev2, gossip.MODE_CSR, 0, part=(r, 2)) for r in range(2)]
+    ranks[1].abort()
+    with pytest.raises(gossip.GossipError, match="aborted"):
+        gossip.group_run(ranks)
+    with pytest.raises(gossip.GossipError, match="aborted"):
+        ranks[1].tick_begin()
+    for r in ranks:
+        r.close()
+
+
 def test_row_partition_needs_an_exchange(gossip):
     n = 1100
     topo, t_cut, ev = _inputs(gossip, n, 0.02, 51, 6.0)
@@ -188,3 +216,9 @@ def test_rehearse_rows_keeps_results(gossip):
         assert np.array_equal(getattr(got, k), getattr(w, k)), k
     assert rh["ticks"] > 100 and (rh["pull_ms"] > 0).all() and (rh["msg_bytes"] > 0).all()
     assert (rh["pack_ms"] > 0).all() and (rh["unpack_ms"] > 0).all()
+    # a rehearsal engine is unpartitioned: set_row_partition after the option is refused too
+    e = gossip.Engine(n, L, T0, t_cut)
+    e.set_option("rehearse_rows", 3)
+    with pytest.raises(gossip.GossipError, match="rehearse_rows"):
+        e.set_row_partition(0, 2)
+    e.close()

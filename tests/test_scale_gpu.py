@@ -154,7 +154,8 @@ def test_c4_sample_matches_oracle_a(gossip, oracle, c4):
         ("young-tile slots forced on", (("young", 1),)),
         ("young tiles, 8-entry slots (overflow paths at scale)", (("young", 1), ("young_cap", 8))),
         ("young tiles after k_pull on one stream", (("young", 1), ("young_overlap", 0))),
-        ("nt rows, 16384-block grid (the C4 production kernel)", (("pull_nt", 1), ("pull_grid", 16384))),
+        ("nt rows, 16384-block grid (k_pull<8..16,1,false>: this sample's window is <= 16 words; "
+         "the production k_pull<32,1,true> is test_c4_headline_kernels_match_oracle_b's)", (("pull_nt", 1), ("pull_grid", 16384))),
         ("nt rows, 3-block grid", (("pull_nt", 1), ("pull_grid", 3))),
         ("every live seen pair read (no occupancy gate)", (("pull_gate", 0),)),
         ("no bottom-up early exit (late_age 0; the default exits on every tile)", (("late_age", 0),)),
@@ -175,6 +176,61 @@ def test_c4_sample_matches_oracle_a(gossip, oracle, c4):
     tot = _sum(parts)
     for k in SUM_STATS:
         assert np.array_equal(tot[k], getattr(ref, k).astype(np.uint64)), ("2 shards", k)
+
+
+def _c4_headline_sample(gossip, c4, per_tick=20, ticks=24):
+    """Distinct-id generations of the bench's slice: `per_tick` of every tick of [2000, 2000 +
+    ticks), evenly spaced in the tick's (ns, node) order; floods cut ~6 hops after the last tick."""
+    W = _w()
+    n = c4[0].num_nodes
+    L, T = W.L_NS, W.SLICE_NS
+    ev, _ = W.slice_schedule(n, W.CONFIGS["C4"]["node_seed"], T, T + ticks * L)
+    win = ev[ev["ns"] >= T]
+    # ids that occur once in the slice (ORACLE B covers distinct ids only)
+    ids, cnt = np.unique(ev["share_id"], return_counts=True)
+    win = win[np.isin(win["share_id"], ids[cnt == 1])]
+    tick = win["ns"] // L
+    pick = []
+    for k in range(T // L, T // L + ticks):
+        idx = np.flatnonzero(tick == k)
+        pick.append(idx[np.linspace(0, len(idx) - 1, per_tick).astype(np.int64)])
+    out = np.ascontiguousarray(win[np.concatenate(pick)])
+    assert len(np.unique(out["share_id"])) == len(out) == per_tick * ticks
+    return out, T + (ticks + 6) * L + L // 2
+
+
+def test_c4_headline_kernels_match_oracle_b(gossip, oracle, c4):
+    # The kernels that produce the bench's number, in the bench's configuration: k_pull<32,1,true>
+    # (windows > 64 words: 32 word-lanes per node, non-temporal rows, tile lists in age order, the
+    # 16,384-block grid, the early exit on every tile, saturation bits, dense-row tiles) beside
+    # k_pull_young (young_nt slot reads, concurrent on the second stream) -- on the C4 graph against
+    # ORACLE B (p2pnode.cc:127-199).  A fresh tile per tick (F_TILE_PER_TICK) gives the window of ~25
+    # tiles those kernels need at a CPU-checkable 480 generations; young tiles and NT rows are forced
+    # (auto keys them off the slice's full ~14k births per tick); dense rows are forced on every
+    # listed tile (auto: a 20-share tile's rows are not dense) and off.
+    W = _w()
+    topo = c4[0]
+    n = topo.num_nodes
+    ev, t_cut = _c4_headline_sample(gossip, c4)
+    a, b = topo.links()
+    ref = oracle.run_oracle_b(n, W.L_NS, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], threads=16)
+    del a, b
+    assert ref.edge_events > 1e10
+    prod = (("young", 1), ("young_nt", 1), ("pull_nt", 1), ("pull_grid", 16384), ("pull_tile_order", 1))
+    variants = [
+        ("production kernels, dense rows auto", prod),
+        ("production kernels, dense rows on every listed tile", prod + (("dense_rows", 1),)),
+        ("production kernels, no saturation bits, no dense rows", prod + (("pull_sat", 0), ("dense_rows", 0))),
+    ]
+    for name, opts in variants:
+        st, c = _run(gossip, topo, ev, W.T0_NS, t_cut, options=opts, flags=gossip.F_TILE_PER_TICK)
+        _same(st, ref, what=name)
+        assert c.edge_events == ref.edge_events, name
+        # the instantiation: k_pull<32, 1, true> over tile lists, early exit on, k_pull_young ran
+        assert c.words_hw > 64 and c.pull_lpw == 32 and c.pull_nt == 1 and c.pull_grid == 16384, name
+        assert c.pull_tiles == 1 and c.pull_late_age == 1 and c.young_launches > 0, name
+        if dict(opts).get("pull_sat", 1):
+            assert c.pull_sat == 1 and c.pull_sat_skips > 0, name
 
 
 def _c4_shard_deltas(gossip, topo, ev, shard, shards, t0, t1):

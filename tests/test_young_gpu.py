@@ -66,16 +66,30 @@ def test_young_sparse_4096(gossip, oracle, cap, age):
 
 
 @pytest.mark.parametrize("cap,id_mask", [(3, 0), (127, 0), (127, 0x3FF)])
-def test_young_own_frontier_dedup(gossip, oracle, cap, id_mask):
-    # young_own 1: incoming bits deduped against the node's own frontier of the last two ticks
-    # (its own slots); seen is read only for id-group words and overflowed nodes
+def test_young_seen_lists(gossip, oracle, cap, id_mask):
+    # seen lists (young_kernel.h): a node's seen bits of its young tiles as list entries (read with
+    # the peers' slots, applied as AND-NOT, whole groups), materialised into dense seen rows when a
+    # tile leaves the young set -- no dense seen word is read while no list overflows
     c = _parity(gossip, oracle, 3000, 12.0 / 2999, 81, 6.0, 5.0,
-                dict(young_cap=cap, young_age=4, young_own=1), id_mask=id_mask, flags=gossip.F_TILE_PER_TICK)
-    assert c.young_seen_writes > 0
-    if not id_mask and c.young_fallback_rows == 0:  # no id group, no overflowed slot: no seen read
-        assert c.young_seen_reads == 0
-    if cap == 3:
-        assert c.young_fallback_rows > 0 and c.young_seen_reads > 0  # overflowed nodes read seen
+                dict(young_cap=cap, young_age=4), id_mask=id_mask, flags=gossip.F_TILE_PER_TICK)
+    assert c.young_list_lines > 0 and c.young_fresh_lines > 0  # lists read/written, rows materialised
+    if not id_mask:
+        assert c.young_seen_reads == 0 and c.young_seen_writes == 0
+
+
+@pytest.mark.parametrize("list_cap,id_mask", [(4, 0x3FF), (12, 0), (127, 0)])
+def test_young_seen_list_overflow(gossip, oracle, list_cap, id_mask):
+    # lists that overflow -- in k_pull_young (more entries than it may keep) and in k_births (a
+    # birth, or a whole id group, that does not fit): the node's young seen rows are materialised
+    # and it dedups against dense seen words from then on (fresh tiles cleared at that node).
+    # 127: 20,000 nodes, the young set covering every node's 6-hop neighbourhood -- ~170 entries
+    if list_cap == 127:
+        c = _parity(gossip, oracle, 20000, 16.0 / 19999, 83, 5.4, 5.0, dict(young_age=6), trace=False,
+                    flags=gossip.F_TILE_PER_TICK)
+    else:
+        c = _parity(gossip, oracle, 400, 0.01, 73, 15.0, 5.0, dict(young_cap=8, young_age=4, young_list_cap=list_cap),
+                    id_mask=id_mask, flags=gossip.F_TILE_PER_TICK)
+    assert c.young_seen_reads > 0 and c.young_list_lines > 0  # some lists overflowed
 
 
 @pytest.mark.parametrize("cap", [2, 127])
@@ -112,6 +126,43 @@ def test_young_periodic_snapshots(gossip, oracle, monkeypatch):
     sim.CreateRandomTopology(8.0 / 1199, 5.0)
     st = sim.Start(21.0)
     assert sim.engine.counters().young_launches > 0
+    ref = oracle.run_reference(num_nodes=1200, connection_prob=8.0 / 1199, sim_time_s=21.0,
+                               topo_seed=77, node_seed=78)
+    for k in STATS:
+        assert np.array_equal(getattr(st, k), getattr(ref, k)), k
+    got = [(gossip.seconds_to_ns(t), g, p, s) for t, g, p, s in sim.periodic]
+    assert got == [tuple(x) for x in ref.periodic]
+
+
+@pytest.mark.parametrize("case", ["overflow", "collisions", "odd_cut", "shared_tiles"])
+def test_young_dense_rows(gossip, oracle, case):
+    # dense-row tiles (pull_kernel.h) beside young tiles: k_pull_young writes every row of a tile
+    # leaving the young set (YT_DW), k_pull reads it next tick without occupancy words -- with
+    # overflowed slots, id-group births, an in-tick cut and tiles shared by several ticks
+    dr = dict(dense_rows=1)
+    if case == "overflow":
+        c = _parity(gossip, oracle, 4096, 16.0 / 4095, 71, 6.0, 5.0, dict(dr, young_cap=1, young_age=3),
+                    flags=gossip.F_TILE_PER_TICK)
+        assert c.young_fallback_rows > 0 and c.pull_dense_tiles >= 0
+    elif case == "collisions":
+        _parity(gossip, oracle, 400, 0.01, 73, 15.0, 5.0, dict(dr, young_cap=2, young_age=4),
+                id_mask=0x3FF, flags=gossip.F_TILE_PER_TICK)
+    elif case == "odd_cut":
+        _parity(gossip, oracle, 3000, 10.0 / 2999, 75, 7.37, 2.3, dict(dr, young_cap=16, young_age=3),
+                flags=gossip.F_TILE_PER_TICK)
+    else:
+        _parity(gossip, oracle, 600, 0.008, 74, 12.0, 5.0, dict(dr, young_cap=4, young_age=5), id_mask=0x7FF)
+
+
+def test_young_dense_rows_periodic_snapshots(gossip, oracle, monkeypatch):
+    # periodic snapshot partials with dense-row tiles and saturation bits in play
+    monkeypatch.setenv("GOSSIP_YOUNG", "1")
+    monkeypatch.setenv("GOSSIP_DENSE_ROWS", "1")
+    sim = gossip.P2PGossipNetworkSimulation(1200, topo_seed=77, node_seed=78, flags=gossip.F_TILE_PER_TICK)
+    sim.CreateRandomTopology(8.0 / 1199, 5.0)
+    st = sim.Start(21.0)
+    c = sim.engine.counters()
+    assert c.young_launches > 0 and c.pull_sat == 1
     ref = oracle.run_reference(num_nodes=1200, connection_prob=8.0 / 1199, sim_time_s=21.0,
                                topo_seed=77, node_seed=78)
     for k in STATS:
