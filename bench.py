@@ -250,7 +250,8 @@ def rehearse_rows(args, wl, topo, ev, shards, R, flags):
         "rank_ingress_bytes_per_tick": ingress.tolist(),
         "rank_ingress_bytes_per_tick_max": float(ingress.max()),
         "unpartitioned_pull_ms_per_tick": c1.pull_ms / max(c1.pull_launches, 1),
-        "rank_device_gib": (fbytes + c1.words_cap * 8 * int(own_rows.max())) / 2**30,
+        # + the exchange buffers a rank would hold: its own message and the R - 1 it receives
+        "rank_device_gib": (fbytes + c1.words_cap * 8 * int(own_rows.max()) + R * float(msg.max())) / 2**30,
         "wall_s_rehearsal": wall,
         "window_words": c1.words_hw,
     }
@@ -269,8 +270,6 @@ def main():
     ap.add_argument("--cpu-hops", type=int, default=6, help="hops the CPU-sample floods run")
     ap.add_argument("--noskip", action="store_true",
                     help="diagnostic: dense pull (every peer-row word read) for PMC calibration")
-    ap.add_argument("--pull-kernel", choices=("auto", "wide", "generic"), default="auto",
-                    help="diagnostic: force the scalar-peer (wide) or lane-shuffle (generic) pull")
     ap.add_argument("--rehearse-shards", type=int, default=0,
                     help="diagnostic: run only shard 0 of S on this one GPU (per-rank footprint "
                          "and time of an S-GPU run); the JSON line is marked REHEARSAL")
@@ -319,7 +318,6 @@ def main():
     ev, sinfo = WL.slice_schedule(n, WL.CONFIGS[args.workload]["node_seed"], SLICE_NS, t_gen_end,
                                   threads=args.threads)
     flags = gossip.F_TIMING | (gossip.F_NOSKIP if args.noskip else 0)
-    flags |= {"auto": 0, "wide": gossip.F_WIDE_PULL, "generic": gossip.F_GENERIC_PULL}[args.pull_kernel]
     if rank == 0:
         rp, _, _ = topo.csr()
         log(f"[bench] {wl['desc']}: {topo.num_nodes} nodes, {int(rp[-1])} directed entries, "

@@ -160,8 +160,8 @@ typedef struct gossip_config {
 #define GOSSIP_F_TIMING 2u /* time each pull-kernel launch with HIP events          */
 #define GOSSIP_F_NOSKIP 4u /* diagnostic: dense pull (no dead/saturated skipping);
                               results are identical, only the bytes read change       */
-#define GOSSIP_F_WIDE_PULL 8u     /* test: scalar-peer wide pull kernel at every window width */
-#define GOSSIP_F_GENERIC_PULL 16u /* diagnostic: lane-shuffle pull kernel at every width     */
+/* (flag values 8 and 16 -- the round-1 scalar-peer pull kernel and its opposite -- are retired
+ *  and ignored) */
 #define GOSSIP_F_TILE_PER_TICK 32u /* test: open a fresh 1024-share tile every tick (wide,
                                       sparsely filled windows at small n)                 */
 #define GOSSIP_F_HOP_BATCH 128u /* hop-batched run: generation g of every node is simulated in

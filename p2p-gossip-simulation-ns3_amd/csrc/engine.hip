@@ -1350,10 +1350,11 @@ int gossip_engine::grow(uint32_t new_stride) {
             d_nz[k] = q;
         }
         device_bytes += 16ull * n * (new_ntw - ntw);
-        if (d_sat) {  // (a cache: zeros = nothing saturated)
-            HIP_TRY(hipFree(d_sat));
-            HIP_TRY(hipMalloc(&d_sat, (size_t)n * new_ntw * 8));
-            HIP_TRY(hipMemset(d_sat, 0, (size_t)n * new_ntw * 8));
+        for (unsigned long long** sp : {&d_sat}) {  // (a cache: zeros = nothing saturated)
+            if (!*sp) continue;
+            HIP_TRY(hipFree(*sp));
+            HIP_TRY(hipMalloc(sp, (size_t)n * new_ntw * 8));
+            HIP_TRY(hipMemset(*sp, 0, (size_t)n * new_ntw * 8));
             device_bytes += 8ull * n * (new_ntw - ntw);
         }
         ntw = new_ntw;
@@ -1769,8 +1770,10 @@ int gossip_engine::tick_step_a(int64_t t) {
     //     nothing; a pass then never spends its lanes on them.
     pt_off.clear();
     pt_cnt.clear();
-    const bool use_ptile = opt_pull_tiles && !dense && !(cfg.flags & (GOSSIP_F_NOSKIP | GOSSIP_F_WIDE_PULL)) && hw;
+    const bool use_ptile = opt_pull_tiles && !dense && !(cfg.flags & GOSSIP_F_NOSKIP) && hw;
     pt_used = use_ptile;
+    const bool sat_on = use_ptile && opt_pull_sat != 0 && !(cfg.flags & GOSSIP_F_NOSKIP) && d_sat;
+    const bool dr_used = use_ptile && opt_dense_rows != 0 && row_count == 1 && !(cfg.flags & GOSSIP_F_NOSKIP);
     if (use_ptile) {
         const uint64_t need = (uint64_t)hw / kTileWords + 16ull * ((hw + kPullLdsWords - 1) / kPullLdsWords) + 16;
         if (need > ptile_cap) {
@@ -1829,8 +1832,7 @@ int gossip_engine::tick_step_a(int64_t t) {
     //     and no birth landed in it since then (a birth adds a live column the bits did not see);
     //   TM_NZ: listed and not dense-row: the tiles that still need their peers' occupancy words.
     // Row partitions keep neither (another rank's rows arrive only where occupied).
-    sat_used = use_ptile && opt_pull_sat != 0 && !(cfg.flags & GOSSIP_F_NOSKIP) && d_sat;
-    const bool dr_used = use_ptile && opt_dense_rows != 0 && row_count == 1 && !(cfg.flags & GOSSIP_F_NOSKIP);
+    sat_used = sat_on;
     last_dense_tiles = 0;
     if (sat_used || dr_used) {
         if (TM_WORDS * ntw > tmask_cap) {
@@ -1853,15 +1855,11 @@ int gossip_engine::tick_step_a(int64_t t) {
             unsigned long long* m = TM + (size_t)TM_WORDS * (tl >> 6);
             const bool fresh = tile_first[tl] == t;
             const bool dr = dr_used && !fresh && tile_dw[tl] == t - 1;
-            if (dr) {
-                m[TM_DENSE] |= bit;
-                last_dense_tiles++;
-            } else {
-                m[TM_NZ] |= bit;
-            }
-            if (sat_used && !fresh && tile_listed[tl] == t - 1 && tile_last_inject[tl] != t - 1 &&
-                tile_inj_prev[tl] != t - 1)
-                m[TM_SATOK] |= bit;
+            if (dr) last_dense_tiles++;
+            m[dr ? TM_DENSE : TM_NZ] |= bit;
+            // sat bits written by k_pull last tick, no birth since
+            const bool clean = !fresh && tile_last_inject[tl] != t - 1 && tile_inj_prev[tl] != t - 1;
+            if (sat_used && clean && tile_listed[tl] == t - 1) m[TM_SATOK] |= bit;
             if (dr_used && dense_row_hop(tl, t - tile_first[tl])) {  // F_cur's hop next tick
                 for (uint32_t q = 0; q < kTileWords; q++) WF[tl * kTileWords + q] |= (uint8_t)WF_DW;
                 tile_dw[tl] = t;
@@ -1984,15 +1982,8 @@ int gossip_engine::tick_step_a(int64_t t) {
                     sat_launches += sat_used;
                 }
                 last_lpw = (uint32_t)lpw;
-                // k_pull_wide (scalar peer loop) is opt-in: on C3 it measured 3.41 ms per launch
-                // against 3.33 ms for the lane-shuffle k_pull<64,1> (profiles/r01/ab_generic.json).
-                const bool wide = split_edges && n < (1u << 24) && !(cfg.flags & GOSSIP_F_GENERIC_PULL) &&
-                                  (cfg.flags & GOSSIP_F_WIDE_PULL);
-                if (wide)
-                    k_pull_wide<<<grid, 256, pull_lds_bytes(c.wact), stream>>>(c);
-                else
-                    launch_pull(lpw, epn, nt_rows, grid, pull_lds_bytes(c.wact, c.keep_lds != 0, c.nptile) + extra_lds,
-                                stream, c);
+                launch_pull(lpw, epn, nt_rows, grid, pull_lds_bytes(c.wact, c.keep_lds != 0, c.nptile) + extra_lds,
+                            stream, c);
             }
         };
         hipEvent_t e0 = nullptr, e1 = nullptr, p0 = nullptr, p1 = nullptr;
@@ -2384,14 +2375,28 @@ DevLayout dev_layout(uint64_t k, uint32_t ntw, uint32_t wlive) {
         NCCL_TRY(x);                                                                        \
     } while (0)
 
+// The exchange's message / receive buffers (row partition) grow with the frontier; they count in
+// device_bytes (the engine's footprint, gossip_counters) and fail cleanly with GOSSIP_ENOMEM --
+// the callers' cue to split the shares into more shards -- when the device or the mem_limit
+// option has no room left, instead of a HIP error mid-run.
 int gossip_engine::ensure_dev(uint64_t*& p, uint64_t& cap, uint64_t words) {
     if (words <= cap) return GOSSIP_OK;
     HIP_TRY(hipStreamSynchronize(stream));  // (rare: growth) both streams may still read p
     if (xstream) HIP_TRY(hipStreamSynchronize(xstream));
+    const uint64_t ncap = std::max<uint64_t>(words, cap + cap / 2);
+    size_t freeb = 0, totalb = 0;
+    HIP_TRY(hipMemGetInfo(&freeb, &totalb));
+    const uint64_t room = (uint64_t)freeb + cap * 8;  // (the old buffer is freed first)
+    if (ncap * 8 > room || (opt_mem_limit > 0 && device_bytes + (ncap - cap) * 8 > (uint64_t)opt_mem_limit))
+        return set_error(GOSSIP_ENOMEM, "row exchange: no device memory for a " + std::to_string(ncap * 8) +
+                                            "-byte message buffer (" + std::to_string(device_bytes) + " bytes held)");
     hipFree(p);
     p = nullptr;
-    cap = std::max<uint64_t>(words, cap + cap / 2);
-    HIP_TRY(hipMalloc(&p, cap * 8));
+    device_bytes -= cap * 8;
+    cap = 0;
+    HIP_TRY(hipMalloc(&p, ncap * 8));
+    cap = ncap;
+    device_bytes += cap * 8;
     return GOSSIP_OK;
 }
 
@@ -3678,6 +3683,11 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
                            5ull * acct[9] +
                            8ull * (acct[11] + acct[12]) + e->young_launches * (8ull * (e->n + 1) + 16ull * e->n);
     c->young_fresh_lines = acct[19];
+#ifdef YOUNG_STAMPS
+    fprintf(stderr, "young_stamps_cycles");
+    for (int k = 20; k < 28; k++) fprintf(stderr, " %llu", (unsigned long long)acct[k]);
+    fprintf(stderr, "\n");
+#endif
     c->young_list_lines = acct[17] + acct[18];
     c->pull_lpw = e->last_lpw;
     c->pull_dense_tiles = e->last_dense_tiles;

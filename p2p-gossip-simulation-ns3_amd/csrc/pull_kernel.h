@@ -148,6 +148,7 @@ __host__ __device__ constexpr size_t pull_lds_bytes(uint32_t wact, bool keep = f
 // + (option pull_sat) the launch's two occupancy words of tmask and every wave's sat words of its
 // 64 nodes (2 per node), behind the rest
 constexpr size_t kPullSatLds = 8u * 8u + 4u * 64u * 2u * 8u;
+static_assert(2u * TM_WORDS <= 8u, "tmask words of a launch fit their LDS slot");
 constexpr uint32_t kNoWord = 0xffffffffu;
 
 // Peer ids of the first GRP peers of item k's node (0xffffffff past the list).
@@ -164,16 +165,8 @@ __device__ __forceinline__ uint32_t pull_cid_load(const PullArgs& a, uint32_t st
     return (c0 + idx < a.n && jj < end) ? (uint32_t)a.col[jj] : 0xffffffffu;
 }
 
-#ifndef PULL_WAVES_PER_EU
-#define PULL_WAVES_PER_EU 0  // A/B builds: cap VGPRs for more waves per SIMD (make variants)
-#endif
-#if PULL_WAVES_PER_EU
-#define PULL_OCC __attribute__((amdgpu_waves_per_eu(PULL_WAVES_PER_EU)))
-#else
-#define PULL_OCC
-#endif
 template <int LPW, int EPN, bool NT = false>
-__global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
+__global__ __launch_bounds__(256) void k_pull(PullArgs a) {
     constexpr int GRP = LPW * EPN;  // lanes per node
     constexpr int NPW = 64 / GRP;   // nodes per wave step
     static_assert(GRP <= 64 && (64 % GRP) == 0, "lane layout");
@@ -262,6 +255,10 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
         PULL_LANES
         const int64_t rp = a.rowptr[min(c0 + lane, n)];
         const int64_t rp_end = a.rowptr[min(c0 + 64u, n)];
+        // |peers| with multiplicity of the chunk's node `lane` (sent += new x deg): loaded with the
+        // row pointers -- a load after a node's stores waits for all of them (vmcnt(0)), and
+        // would drain the item pipeline's prefetches once per node
+        const uint32_t dg = a.deg[min(c0 + lane, n - 1u)];
         if (sat_on) {  // the chunk's sat words, trusted bits only (waited for below)
 #pragma unroll
             for (uint32_t q = 0; q < 2u; q++) {
@@ -503,6 +500,11 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                     acc1 |= (uint64_t)lane_get((uint32_t)acc1, src) | ((uint64_t)lane_get((uint32_t)(acc1 >> 32), src) << 32);
                 }
             }
+            // Everything this item loaded -- the gather's rows and the next items' prefetches -- has
+            // landed before its stores issue: gfx950 counts stores in vmcnt, and the pipeline's
+            // hand-over at the loop latch (s2c = s2n, nz0 = nz1, the ids) would otherwise wait with
+            // the item's stores outstanding (vmcnt(0): a write round trip per item)
+            __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
             // ---- dedup ----
             uint64_t n0 = 0ull, n1 = 0ull;
             if (act && el == 0 && !dead) {
@@ -579,16 +581,14 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
                 }
             }
             // ---- per-node counters after the node's last pass ----
+            // (no-return atomics: nothing waits on them -- a read-modify-write would load, and
+            // that wait drains every prefetch and store in flight)
             if (pass + 1u == npass) {
                 const uint32_t c = group_add<GRP>(cnt, lane);
+                const uint32_t dv = lane_get(dg, idx);  // (whole wave active)
                 if (gl == 0 && c) {
-                    if (a.shared_out) {  // no-return atomics: nothing waits on them
-                        atomicAdd(&a.recv[v], c);
-                        atomicAdd(reinterpret_cast<unsigned long long*>(&a.sent[v]), (unsigned long long)c * a.deg[v]);
-                    } else {
-                        a.recv[v] += c;
-                        a.sent[v] += (uint64_t)c * a.deg[v];
-                    }
+                    atomicAdd(&a.recv[v], c);
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&a.sent[v]), (unsigned long long)c * dv);
                 }
                 cnt = 0;
             }
@@ -620,254 +620,4 @@ __global__ __launch_bounds__(256) PULL_OCC void k_pull(PullArgs a) {
         if (x) atomicOr(&a.live[a.wbase + i], x);
     }
 #undef PULL_LANES
-}
-
-// ------------------------------------------------------------------------------------------
-// k_pull_wide -- the sparse-graph pull for windows wider than 64 words: one node per wave
-// step, lane l = word pair l of a 128-word pass (8 tiles).  The node of an item is
-// wave-uniform, which makes the peer loop scalar:
-//   * lane p holds peer p's id and the occupancy byte of the pass's 8 tiles, packed as
-//     (id << 8 | byte) (needs n < 2^24);
-//   * a ballot compacts the peers that hold an occupied tile the node still needs, and the
-//     gather walks only those: per peer one v_readlane gives the id (a scalar row address,
-//     global_load with an SGPR base) and its tile byte (lanes of other tiles stay idle).
-// Same semantics, work skipping and pipeline as k_pull<LPW, 1>.
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t tiles_any(unsigned long long m) {
-    // bit j = some lane of tile j (lanes 8j .. 8j+7) is set in the lane mask m
-    uint32_t r = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) r |= (((m >> (8 * j)) & 0xffull) != 0ull ? 1u : 0u) << j;
-    return r;
-}
-
-__global__ __launch_bounds__(256) void k_pull_wide(PullArgs a) {
-    extern __shared__ unsigned long long smem[];
-    unsigned long long* s_lp = smem;
-    unsigned long long* s_new = smem + a.wact;
-    uint8_t* s_wf = reinterpret_cast<uint8_t*>(smem + 2u * a.wact);
-    for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
-        const uint8_t f = a.wflags[a.wbase + i];
-        // a young word is k_pull_young's: dead here, no clear, no write
-        s_lp[i] = (f & WF_YOUNG) ? 0ull : (a.live_prev && !a.noskip) ? a.live_prev[a.wbase + i] : ~0ull;
-        s_new[i] = 0ull;
-        s_wf[i] = (f & WF_YOUNG) ? (uint8_t)0 : f;
-    }
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t tl = lane >> 3;  // tile of this lane inside a pass
-    const uint64_t stride = a.stride;
-    const uint64_t n = a.n;
-    const uint64_t wave = (uint64_t)blockIdx.x * 4u + wave_in_block();
-    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
-    const uint32_t npass = (a.wact + 127u) / 128u;
-    const char* Fbytes = reinterpret_cast<const char*>(a.Fcur);
-    unsigned long long snap_local = 0ull;
-    uint32_t t_pe = 0, t_col = 0, t_srd = 0, t_swr = 0, t_fwr = 0, t_nz = 0;  // wave-uniform
-    unsigned long long nzacc = 0ull;  // occupancy bits of the current nz word (uniform)
-
-    // peer ids of node j's first 64 peers (lane = peer); 0xffffffff past the list
-    auto cid_load = [&](uint32_t j, int64_t rp, int64_t rp_end, uint64_t c0) -> uint32_t {
-        const int32_t beg = __shfl((int)rp, (int)j, 64);
-        const int32_t nx = __shfl((int)rp, (int)((j + 1u) & 63u), 64);
-        const int32_t end = (j + 1u < 64u) ? nx : (int32_t)rp_end;
-        const int32_t jj = beg + (int32_t)lane;
-        return (c0 + j < n && jj < end) ? (uint32_t)a.col[jj] : 0xffffffffu;
-    };
-
-    for (uint64_t c0 = a.v0 + wave * 64u; c0 < n; c0 += nwaves * 64u) {
-        const int64_t rp = a.rowptr[min(c0 + lane, n)];
-        const int64_t rp_end = a.rowptr[min(c0 + 64u, n)];
-        uint32_t j = 0, pass = 0;  // item = (node c0 + j, pass)
-        ulonglong2 s2c = make_ulonglong2(0ull, 0ull);
-        if (c0 < n && 2u * lane < a.wact && (s_lp[2u * lane] | s_lp[2u * lane + 1u]) != 0ull)
-            s2c = *reinterpret_cast<const ulonglong2*>(a.seen + c0 * stride + a.wbase + 2u * lane);
-        uint32_t cid0 = cid_load(0u, rp, rp_end, c0);
-        uint32_t cid1 = npass > 1u ? cid0 : cid_load(1u, rp, rp_end, c0);
-        unsigned long long nz0 = cid0 != 0xffffffffu ? a.nz_cur[(uint64_t)cid0 * a.ntw + (a.wbase >> 10)] : 0ull;
-        t_nz += wave_count(cid0 != 0xffffffffu);
-        uint32_t cnt = 0;
-        while (j < 64u) {
-            const uint32_t j1 = pass + 1u < npass ? j : j + 1u;
-            const uint32_t p1 = pass + 1u < npass ? pass + 1u : 0u;
-            const uint32_t j2 = p1 + 1u < npass ? j1 : j1 + 1u;
-            const uint64_t v = c0 + j;
-            const uint32_t lw = pass * 128u + 2u * lane;  // word offset inside the launch
-            const uint32_t w = a.wbase + lw;
-            const bool act = v < n && lw < a.wact;
-            // ---- stage loads: seen pair of item k+1, ids of k+2, occupancy of k+1 ----
-            ulonglong2 s2n = make_ulonglong2(0ull, 0ull);
-            {
-                const uint32_t lw1 = p1 * 128u + 2u * lane;
-                if (j1 < 64u && c0 + j1 < n && lw1 < a.wact && (s_lp[lw1] | s_lp[lw1 + 1u]) != 0ull)
-                    s2n = *reinterpret_cast<const ulonglong2*>(a.seen + (c0 + j1) * stride + a.wbase + lw1);
-            }
-            uint32_t cid2 = 0xffffffffu;
-            if (j2 < 64u) cid2 = j2 == j1 ? cid1 : cid_load(j2, rp, rp_end, c0);
-            unsigned long long nz1 = 0ull;
-            if (j1 < 64u) {
-                const uint32_t tw1 = (a.wbase + p1 * 128u) >> 10;
-                if (j1 == j && tw1 == (w - 2u * lane) >> 10) {
-                    nz1 = nz0;
-                } else {
-                    nz1 = cid1 != 0xffffffffu ? a.nz_cur[(uint64_t)cid1 * a.ntw + tw1] : 0ull;
-                    t_nz += wave_count(cid1 != 0xffffffffu);
-                }
-            }
-            // ---- decide ----
-            uint32_t f0 = 0, f1 = 0;
-            uint64_t lp0 = 0ull, lp1 = 0ull;
-            if (act) {
-                const uint16_t fl = *reinterpret_cast<const uint16_t*>(s_wf + lw);
-                f0 = fl & 0xffu;
-                f1 = fl >> 8;
-                lp0 = s_lp[lw];
-                lp1 = s_lp[lw + 1u];
-            }
-            const bool dead = (lp0 | lp1) == 0ull;
-            ulonglong2 s2 = s2c;
-            if (f0 & WF_CLEAR) s2.x = 0ull;
-            if (f1 & WF_CLEAR) s2.y = 0ull;
-            uint64_t k0 = ~0ull, k1 = ~0ull;
-            if (act && (f0 & WF_KEEP)) k0 = a.ctl[w].keep;
-            if (act && (f1 & WF_KEEP)) k1 = a.ctl[w + 1].keep;
-            const bool need = act && !dead &&
-                              (a.noskip || ((lp0 & ~s2.x & k0) | (lp1 & ~s2.y & k1)) != 0ull);
-            const uint32_t tneed = tiles_any(__ballot(need));  // tiles whose peer rows are worth reading
-            // ---- gather: only peers with an occupied tile the node needs ----
-            uint64_t acc0 = 0ull, acc1 = 0ull;
-            if (tneed) {
-                const int32_t beg = __builtin_amdgcn_readlane((int)rp, (int)j);
-                const int32_t end = j < 63u ? __builtin_amdgcn_readlane((int)rp, (int)(j + 1u)) : (int32_t)rp_end;
-                const uint32_t tile0 = ((w - 2u * lane) >> 4) & 63u;  // first tile of the pass in its nz word
-                const uint32_t off = w * 8u;                          // byte offset of the pair in a row
-                for (int32_t cb = beg; cb < end; cb += 64) {
-                    uint32_t cid = cid0;
-                    unsigned long long nzw = nz0;
-                    if (cb != beg) {  // peers beyond the first 64: loaded inline (rare)
-                        const int32_t jj = cb + (int32_t)lane;
-                        cid = jj < end ? (uint32_t)a.col[jj] : 0xffffffffu;
-                        nzw = cid != 0xffffffffu ? a.nz_cur[(uint64_t)cid * a.ntw + (w >> 10)] : 0ull;
-                        t_nz += wave_count(cid != 0xffffffffu);
-                    }
-                    const bool valid = (int32_t)lane < end - cb;
-                    t_col += wave_count(valid);
-                    const uint32_t zb = valid ? ((uint32_t)(nzw >> tile0) & 0xffu) : 0u;
-                    const uint32_t pk = (cid << 8) | zb;
-                    unsigned long long todo = __ballot((zb & tneed) != 0u);
-                    while (todo) {
-                        ulonglong2 q[kInflight];
-                        bool h[kInflight];
-#pragma unroll
-                        for (int i = 0; i < kInflight; i++) {
-                            q[i] = make_ulonglong2(0ull, 0ull);
-                            h[i] = false;
-                            if (todo) {
-                                const int t = __builtin_ctzll(todo);
-                                todo &= todo - 1ull;
-                                const uint32_t pt = (uint32_t)__builtin_amdgcn_readlane((int)pk, t);
-                                const uint32_t hb = pt & tneed;
-                                t_pe += 8u * (uint32_t)__builtin_popcount(hb);
-                                h[i] = (hb >> tl) & 1u;
-                                const char* row = Fbytes + (uint64_t)(pt >> 8) * stride * 8u;
-                                if (h[i]) q[i] = *reinterpret_cast<const ulonglong2*>(row + off);
-                            }
-                        }
-#pragma unroll
-                        for (int i = 0; i < kInflight; i++) {
-                            acc0 |= q[i].x;
-                            acc1 |= q[i].y;
-                        }
-                    }
-                }
-            }
-            // ---- dedup ----
-            uint64_t n0 = 0ull, n1 = 0ull;
-            if (act && !dead) {
-                n0 = acc0 & ~s2.x & k0;
-                n1 = acc1 & ~s2.y & k1;
-                if (f0 & WF_GROUP) n0 = group_fix(n0, s2.x, a.ctl[w].gmask, a.ctl[w].gstart);
-                if (f1 & WF_GROUP) n1 = group_fix(n1, s2.y, a.ctl[w + 1].gmask, a.ctl[w + 1].gstart);
-            }
-            const unsigned long long anynew = __ballot((n0 | n1) != 0ull || (a.noskip && act));
-            const bool ta = ((anynew >> (lane & ~7u)) & 0xffull) != 0ull;  // tile row written
-            // ---- state, counters ----
-            const bool swr = act && (dead ? ((f0 | f1) & WF_CLEAR) != 0u
-                                          : ((n0 | n1) != 0ull || ((f0 | f1) & WF_CLEAR) != 0u));
-            t_fwr += wave_count(act && ta);
-            t_srd += wave_count(act && !dead);
-            t_swr += wave_count(swr);
-            if (act) {
-                uint64_t* sp = a.seen + v * stride + w;
-                uint64_t* fp = a.Fnext + v * stride + w;
-                if (ta) *reinterpret_cast<ulonglong2*>(fp) = make_ulonglong2(n0, n1);
-                if (swr) {
-                    if (dead && !((f0 & f1) & WF_CLEAR))
-                        sp[(f0 & WF_CLEAR) ? 0 : 1] = 0ull;
-                    else
-                        *reinterpret_cast<ulonglong2*>(sp) = make_ulonglong2(s2.x | n0, s2.y | n1);
-                }
-                if (!dead) {
-                    cnt += (uint32_t)(__popcll(n0) + __popcll(n1));
-                    if (a.snap) {
-                        if (f0 & WF_SNAP) snap_local += (unsigned long long)__popcll(n0 & a.ctl[w].snap);
-                        if (f1 & WF_SNAP) snap_local += (unsigned long long)__popcll(n1 & a.ctl[w + 1].snap);
-                    }
-                    if (n0) atomicOr(&s_new[lw], (unsigned long long)n0);
-                    if (n1) atomicOr(&s_new[lw + 1u], (unsigned long long)n1);
-                }
-            }
-            // ---- occupancy word of the node: 8 tile bits per pass, written once per word ----
-            {
-                const uint32_t pw = a.wbase + pass * 128u;  // first word of the pass
-                const uint32_t tw = pw >> 10;
-                nzacc |= (unsigned long long)tiles_any(__ballot(act && ta)) << ((pw >> 4) & 63u);
-                if (pass + 1u == npass || ((pw + 128u) >> 10) != tw) {
-                    if (lane == 0 && v < n) {
-                        if (!a.shared_out)
-                            a.nz_next[v * a.ntw + tw] = nzacc;
-                        else if (nzacc)
-                            atomicOr(&a.nz_next[v * a.ntw + tw], nzacc);
-                    }
-                    nzacc = 0ull;
-                }
-            }
-            // ---- per-node counters after the node's last pass ----
-            if (pass + 1u == npass) {
-                const uint32_t c = (uint32_t)wave_sum((unsigned long long)cnt);
-                if (lane == 0 && c && v < n) {
-                    if (a.shared_out) {
-                        atomicAdd(&a.recv[v], c);
-                        atomicAdd(reinterpret_cast<unsigned long long*>(&a.sent[v]), (unsigned long long)c * a.deg[v]);
-                    } else {
-                        a.recv[v] += c;
-                        a.sent[v] += (uint64_t)c * a.deg[v];
-                    }
-                }
-                cnt = 0;
-            }
-            s2c = s2n;
-            cid0 = cid1;
-            cid1 = cid2;
-            nz0 = nz1;
-            j = j1;
-            pass = p1;
-        }
-    }
-    if (a.snap) {
-        snap_local = wave_sum(snap_local);
-        if (lane == 0 && snap_local) atomicAdd(a.snap, snap_local);
-    }
-    if (a.acct && lane == 0) {
-        const uint32_t tv[6] = {t_pe, t_col, t_srd, t_swr, t_fwr, t_nz};
-        const int slot_of[6] = {0, 1, 2, 3, 4, 7};
-#pragma unroll
-        for (int q = 0; q < 6; q++)
-            if (tv[q]) acct_add(a.acct, (uint32_t)slot_of[q], (unsigned long long)tv[q]);
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
-        const unsigned long long x = s_new[i];
-        if (x) atomicOr(&a.live[a.wbase + i], x);
-    }
 }

@@ -141,14 +141,16 @@ __device__ __forceinline__ uint64_t group_expand(uint64_t x, uint64_t gm, uint64
     return out;
 }
 
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane) {
-    uint32_t s = x;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = lane_get(s, lane - (uint32_t)off);
-        if (lane >= (uint32_t)off) s += y;
-    }
-    return s - x;
+// Inclusive prefix sum over the wave (every lane active), DPP only: row shifts inside each row of
+// 16, then the row broadcasts of lanes 15 and 31 (a ds_bpermute chain costs an LDS round trip a step)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return x;
 }
 
 // Entry j (0..7) of a lane's 16-B piece of a slot line.
@@ -161,8 +163,26 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m, uint32_t l
     return (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-// 256-thread blocks; the register budget of 4 waves per SIMD (5 and 6 spilled: round 3)
-__global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
+// Diagnostic build YOUNG_STAMPS: shader cycles per phase of the node loop (s_memtime), summed
+// over waves into acct[20..27] (engine.hip prints them with the counters); no output depends on them
+#ifdef YOUNG_STAMPS
+#define YSTAMP(k)                                              \
+    do {                                                       \
+        const uint64_t ys_t = __builtin_amdgcn_s_memtime();    \
+        ycyc[k] += ys_t - ylast;                               \
+        ylast = ys_t;                                          \
+    } while (0)
+#else
+#define YSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+
+// 256-thread blocks; the register budget of 4 waves per SIMD (A/B build: YOUNG_MIN_WAVES)
+#ifndef YOUNG_MIN_WAVES
+#define YOUNG_MIN_WAVES 4
+#endif
+__global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a) {
     extern __shared__ unsigned long long smem[];
     const uint32_t nrw = a.nr * 16u;  // accumulated words
     const uint32_t accw = nrw + kYoungSpare;
@@ -194,29 +214,39 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
     // unhinted second lines, seen-list lines read / written, seen rows materialised / cleared
     uint32_t t_sl = 0, t_col = 0, t_fb = 0, t_srd = 0, t_swr = 0, t_rw = 0, t_slw = 0, t_miss = 0;
     uint32_t t_lr = 0, t_lw = 0, t_mat = 0;
+#ifdef YOUNG_STAMPS
+    uint64_t ycyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t ylast = __builtin_amdgcn_s_memtime();
+#endif
 
     for (uint64_t c0 = a.v0 + wave * 64u; c0 < a.n; c0 += nwaves * 64u) {
         const uint32_t lane = opaque(lane_id);
         const uint32_t cnt_nodes = (uint32_t)min<uint64_t>(64u, a.n - c0);
         const int64_t rp = a.rowptr[c0 + min(lane, cnt_nodes)];
         const int64_t rp_end = a.rowptr[c0 + cnt_nodes];
+        // |peers| with multiplicity of node j in lane j (sent += c x deg): loaded with the row
+        // pointers, not after the node's stores (a load there waits for all of them, vmcnt(0))
+        const uint32_t dg = a.deg[c0 + min(lane, cnt_nodes - 1u)];
         // peer ids of node j (lane p = peer p of its first 64), one node ahead of the gather
         // (the peer's id and its hint byte, combined only when the node's gather starts: bit 31
         // of the id says the peer's slot has a second line -- ids are < 2^31)
-        auto load_ids = [&](uint32_t j, uint32_t& hint) -> uint32_t {
+        auto load_ids = [&](uint32_t j, uint32_t& hint, int32_t& rv) -> uint32_t {
             const int32_t b = (int32_t)lane_read((uint32_t)rp, j & 63u);
             const int32_t nx = (int32_t)lane_read((uint32_t)rp, (j + 1u) & 63u);
             const int32_t e = j + 1u < 64u ? nx : (int32_t)rp_end;
             hint = 0u;
+            rv = -1;
             if (!(j < cnt_nodes && (int32_t)lane < e - b)) return 0xffffffffu;
             hint = a.hint_cur[b + (int32_t)lane];
+            rv = a.rev[b + (int32_t)lane];  // (for the node's second-line hints, if it writes two lines)
             return (uint32_t)a.col[b + (int32_t)lane];
         };
         auto with_hint = [&](uint32_t id, uint32_t hint) -> uint32_t {
             return (id != 0xffffffffu && hint == a.stamp_cur) ? id | 0x80000000u : id;
         };
         uint32_t h_cur = 0u;
-        uint32_t cid_cur = load_ids(0u, h_cur);
+        int32_t rv_cur = -1;
+        uint32_t cid_cur = load_ids(0u, h_cur, rv_cur);
         cid_cur = with_hint(cid_cur, h_cur);
         for (uint32_t jn = 0; jn < cnt_nodes; jn++) {
             const uint32_t lane = opaque(lane_id);
@@ -317,12 +347,13 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
             t_col += (uint32_t)max(0, end - beg);
             unsigned long long ovf = 0ull;
             issue(cid_cur, 0);
-            // own seen list (lanes 0-15: its two lines), with the first batch
-            ulonglong2 ql = make_ulonglong2(~0ull, ~0ull);
-            if (lane < 16u) ql = *reinterpret_cast<const ulonglong2*>(a.list + v * kListU16 + lane * 8u);
+            // own seen list (its two lines, 2 entries per lane), with the first batch
+            const uint32_t ql = reinterpret_cast<const uint32_t*>(a.list + v * kListU16)[lane];
             t_lr += 2u;
             uint32_t h_next = 0u;
-            const uint32_t cid_next = load_ids(jn + 1u, h_next);  // the next node's peers
+            int32_t rv_next = -1;
+            const uint32_t cid_next = load_ids(jn + 1u, h_next, rv_next);  // the next node's peers
+            YSTAMP(0);
             consume(cid_cur, 0, np0, ovf);
             for (int32_t pb = 8 * kYoungQ; pb < np0; pb += 8 * kYoungQ) {  // degree > 8 kYoungQ
                 issue(cid_cur, pb);
@@ -343,22 +374,26 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
                 }
                 fallback(cid, ovf2);
             }
+            YSTAMP(1);
             // ---- seen list: clear the incoming bits the node already holds (p2pnode.cc:189) ----
-            const uint32_t lhdr = lane_read((uint32_t)(ql.x & 0xffffull), 0u);
+            const uint32_t lhdr = lane_read(ql & 0xffffu, 0u);
             const bool lovf = lhdr == kListOverflow;  // (uniform) dense seen rows instead
             const uint32_t ltot = lovf ? 0u : (lhdr & 127u);
-            // entry j of this lane's piece: kept into the new list (its tile stays young)
-            uint32_t keepm = 0u;
+            // entry j (0, 1) of this lane's pair (kSlotTomb: none)
+            auto lentry = [&](uint32_t j) -> uint32_t {
+                const uint32_t idx = lane * 2u + j;
+                const uint32_t e = (ql >> (16u * j)) & 0xffffu;
+                return (idx == 0u || idx > ltot || e == kSlotTomb) ? kSlotTomb : e;
+            };
+            uint32_t keepm = 0u;  // bit j: entry j is kept into the new list (its tile stays young)
             reinterpret_cast<uint32_t*>(s_lst)[lane] = 0xffffffffu;  // tombstones
             __builtin_amdgcn_wave_barrier();
-            if (!lovf && lane < 16u) {
+            if (!lovf) {
 #pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const uint32_t idx = lane * 8u + (uint32_t)j;
-                    const uint32_t e = slot_entry(ql, j);
-                    if (idx == 0u || idx > ltot || e == kSlotTomb) continue;
-                    const uint32_t qp = s_ymap[e >> 10];
-                    if (qp >= a.ny) continue;  // (a tile no longer young: dropped)
+                for (uint32_t j = 0; j < 2u; j++) {
+                    const uint32_t e = lentry(j);
+                    const uint32_t qp = e == kSlotTomb ? 0xffu : s_ymap[e >> 10];
+                    if (qp >= a.ny) continue;  // (none, or a tile no longer young: dropped)
                     if (qp < a.nr)
                         atomicAnd(reinterpret_cast<uint32_t*>(s_acc + qp * 16u + ((e >> 6) & 15u)) + ((e >> 5) & 1u),
                                   ~(1u << (e & 31u)));
@@ -369,10 +404,13 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
             uint32_t kept = 0;
             {
                 const uint32_t c = (uint32_t)__builtin_popcount(keepm);
-                uint32_t pos = 1u + wave_excl_scan(c, lane);
-                kept = wave_sum32(c);
-                for (uint32_t m = keepm; m; m &= m - 1u) s_lst[pos++] = (uint16_t)slot_entry(ql, __builtin_ctz(m));
+                const uint32_t incl = wave_incl_scan(c);
+                uint32_t pos = 1u + incl - c;
+                kept = lane_read(incl, 63u);
+                if (keepm & 1u) s_lst[pos++] = (uint16_t)(ql & 0xffffu);
+                if (keepm & 2u) s_lst[pos] = (uint16_t)(ql >> 16);
             }
+            YSTAMP(2);
             __builtin_amdgcn_wave_barrier();
             // ---- touched words -> list ----
             uint32_t ntouch = 0;
@@ -384,87 +422,79 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
                 ntouch += (uint32_t)__popcll(m);
             }
             __builtin_amdgcn_wave_barrier();
-            // ---- dedup (an overflowed list: against the dense seen words, the first 4 x 64 loads
-            //      issued together); new seen entries of the tiles staying young -> s_lst ----
-            uint32_t cnt = 0, cnt_sp = 0;
-            uint32_t total = 1u + kept;  // next free entry of s_lst
-            uint64_t svq[4];
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const uint32_t t = (uint32_t)r * 64u + lane;
-                svq[r] = 0ull;
-                if (lovf && t < ntouch) {
-                    const uint32_t i = s_list[t];
-                    svq[r] = a.seen[v * stride + s_yt[i >> 4].tile * 16u + (i & 15u)];
+            YSTAMP(3);
+            // ---- dedup against the seen list (or, an overflowed list -- rare -- the dense seen
+            //      words; its own instantiation, so no other node waits on those loads); the
+            //      staying tiles' slot entries and new list entries, positions by one wave scan ----
+            reinterpret_cast<uint32_t*>(s_out)[lane] = 0xffffffffu;  // slot staging: tombstones
+            __builtin_amdgcn_wave_barrier();
+            uint32_t cnt = 0;            // new bits (this lane)
+            uint32_t slot_total = 0;     // slot entries (uniform)
+            uint32_t total = 1u + kept;  // next free entry of s_lst (uniform)
+            auto dedup = [&](auto lovf_c) {
+                constexpr bool LO = decltype(lovf_c)::value;
+                for (uint32_t t0 = 0; t0 < ntouch; t0 += 64) {
+                    const uint32_t t = t0 + lane;
+                    const bool valid = t < ntouch;
+                    const uint32_t i = valid ? s_list[t] : 0u;
+                    const YoungTile yt = s_yt[i >> 4];
+                    const uint32_t w = yt.tile * 16u + (i & 15u);
+                    uint64_t x = 0ull, xe = 0ull;
+                    if (valid) {
+                        const uint32_t f = s_wf[i];
+                        uint64_t sv = 0ull;
+                        if constexpr (LO) sv = a.seen[v * stride + w];
+                        // (a list holds every bit of a seen group: the accumulator has none of them)
+                        x = s_acc[i] & ~sv;
+                        if (f & WF_KEEP) x &= a.ctl[w].keep;  // (loaded and used in the branch)
+                        if (f & WF_GROUP) x = group_fix(x, sv, a.ctl[w].gmask, a.ctl[w].gstart);
+                        if constexpr (LO) {
+                            if (x) a.seen[v * stride + w] = sv | x;
+                        }
+                        if (a.snap && (f & WF_SNAP)) snap_local += (unsigned long long)__popcll(x & a.ctl[w].snap);
+                        s_acc[i] = x;  // the node's new bits, for the outputs below
+                        if constexpr (!LO) xe = (f & WF_GROUP) ? group_expand(x, a.ctl[w].gmask, a.ctl[w].gstart) : x;
+                    }
+                    cnt += (uint32_t)__popcll(x);
+                    if constexpr (LO) {
+                        t_srd += wave_count(valid);
+                        t_swr += wave_count(x != 0ull);
+                    }
+                    const bool stay = (yt.flags & YT_WRITE) != 0u;
+                    const uint32_t cs = stay ? (uint32_t)__popcll(x) : 0u;
+                    const uint64_t xl = stay ? xe : 0ull;
+                    const uint32_t cl = (uint32_t)__popcll(xl);
+                    if (__ballot((cs | cl) != 0u)) {  // (uniform)
+                        const uint32_t pk = (cl << 16) | cs, incl = wave_incl_scan(pk), ex = incl - pk;
+                        uint32_t ps = 1u + slot_total + (ex & 0xffffu), pl = total + (ex >> 16);
+                        const uint32_t tot = lane_read(incl, 63u);
+                        slot_total += tot & 0xffffu;
+                        total += tot >> 16;
+                        for (uint64_t m = cs ? x : 0ull; m; m &= m - 1ull, ps++)
+                            if (ps < kSlotU16)
+                                s_out[ps] = (uint16_t)(((uint32_t)yt.w_idx << 10) | ((i & 15u) << 6) | (uint32_t)__builtin_ctzll(m));
+                        for (uint64_t m = xl; m; m &= m - 1ull, pl++)
+                            if (pl < kListU16)
+                                s_lst[pl] = (uint16_t)(((uint32_t)yt.yid << 10) | ((i & 15u) << 6) | (uint32_t)__builtin_ctzll(m));
+                    }
                 }
-            }
-            for (uint32_t t0 = 0; t0 < ntouch; t0 += 64) {
-                const uint32_t t = t0 + lane;
-                const bool valid = t < ntouch;
-                const uint32_t i = valid ? s_list[t] : 0u;
-                const YoungTile yt = s_yt[i >> 4];
-                const uint32_t w = yt.tile * 16u + (i & 15u);
-                uint64_t x = 0ull, xe = 0ull;
-                if (valid) {
-                    const uint32_t f = s_wf[i];
-                    uint64_t* sp = a.seen + v * stride + w;
-                    const uint32_t r = t0 >> 6;
-                    const uint64_t sv = !lovf ? 0ull : r == 0 ? svq[0] : r == 1 ? svq[1] : r == 2 ? svq[2] : r == 3 ? svq[3] : *sp;
-                    const uint64_t keep = (f & WF_KEEP) ? a.ctl[w].keep : ~0ull;
-                    x = s_acc[i] & ~sv & keep;
-                    // (a list holds every bit of a seen group: the accumulator has none of them)
-                    if (f & WF_GROUP) x = group_fix(x, sv, a.ctl[w].gmask, a.ctl[w].gstart);
-                    if (lovf && x) *sp = sv | x;
-                    if (a.snap && (f & WF_SNAP)) snap_local += (unsigned long long)__popcll(x & a.ctl[w].snap);
-                    s_acc[i] = x;  // the node's new bits, for the outputs below
-                    xe = (f & WF_GROUP) ? group_expand(x, a.ctl[w].gmask, a.ctl[w].gstart) : x;
-                }
-                cnt += (uint32_t)__popcll(x);
-                if (yt.flags & YT_WRITE) cnt_sp += (uint32_t)__popcll(x);
-                t_srd += wave_count(lovf && valid);
-                t_swr += wave_count(lovf && x != 0ull);
-                // the list's new entries (tiles staying young), positions by a wave prefix sum
-                uint64_t xl = (!lovf && (yt.flags & YT_WRITE)) ? xe : 0ull;
-                const uint32_t c = (uint32_t)__popcll(xl);
-                uint32_t pos = total + wave_excl_scan(c, lane);
-                total += wave_sum32(c);
-                while (xl) {
-                    const uint32_t bb = (uint32_t)__builtin_ctzll(xl);
-                    xl &= xl - 1ull;
-                    if (pos < kListU16)
-                        s_lst[pos] = (uint16_t)(((uint32_t)yt.yid << 10) | ((i & 15u) << 6) | bb);
-                    pos++;
-                }
-            }
+            };
+            if (lovf)
+                dedup(std::true_type{});
+            else
+                dedup(std::false_type{});
             const uint32_t lcount = total - 1u;
             const bool lspill = !lovf && lcount > a.list_cap;  // (uniform) the list overflows now
             __builtin_amdgcn_wave_barrier();
+            YSTAMP(4);
             cid_cur = with_hint(cid_next, h_next);  // (arrived long ago: the wait is before the stores)
-            // ---- output: slot entries, or dense rows (overflowed / leaving the young set) ----
-            const uint32_t slot_total = wave_sum32(cnt_sp);
+            const int32_t rv = rv_cur;
+            rv_cur = rv_next;
+            // ---- output: the slot (staged above; an overflowed slot's entries are a subset of its
+            //      dense rows), whole lines (no partial-line writes; unused entries are tombstones:
+            //      readers scatter whole lines), dense rows (overflowed / leaving the young set) ----
             const bool overflow = slot_total > a.cap;
             uint16_t* out = a.slot_next + v * kSlotU16;
-            // the slot is staged in LDS and written as whole lines (no partial-line writes); every
-            // unused entry is a tombstone (readers scatter whole lines)
-            reinterpret_cast<uint32_t*>(s_out)[lane] = 0xffffffffu;
-            __builtin_amdgcn_wave_barrier();
-            if (!overflow && slot_total) {
-                uint32_t base = 1;
-                for (uint32_t t0 = 0; t0 < ntouch; t0 += 64) {
-                    const uint32_t t = t0 + lane;
-                    const uint32_t i = t < ntouch ? s_list[t] : 0u;
-                    const YoungTile yt = s_yt[i >> 4];
-                    uint64_t x = (t < ntouch && (yt.flags & YT_WRITE)) ? s_acc[i] : 0ull;
-                    const uint32_t c = (uint32_t)__popcll(x);
-                    uint32_t pos = base + wave_excl_scan(c, lane);
-                    while (x) {
-                        const uint32_t bb = (uint32_t)__builtin_ctzll(x);
-                        x &= x - 1ull;
-                        s_out[pos++] = (uint16_t)(((uint32_t)yt.w_idx << 10) | ((i & 15u) << 6) | bb);
-                    }
-                    base += wave_sum32(c);
-                }
-            }
             if (lane == 0) s_out[0] = (uint16_t)(overflow ? kSlotOverflow : slot_total);
             __builtin_amdgcn_wave_barrier();
             {
@@ -472,12 +502,15 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
                 if (lane < 8u * lines)
                     *reinterpret_cast<ulonglong2*>(out + lane * 8u) = *reinterpret_cast<const ulonglong2*>(s_out + lane * 8u);
                 t_slw += lines;
-                if (lines == 2u)  // announce the second line to the readers of the next tick
-                    for (int32_t j = beg + (int32_t)lane; j < end; j += 64) {
+                if (lines == 2u) {  // announce the second line to the readers of the next tick
+                    if (rv >= 0) a.hint_next[rv] = (uint8_t)a.stamp_next;  // (the first 64 peers)
+                    for (int32_t j = beg + 64 + (int32_t)lane; j < end; j += 64) {
                         const int32_t r = a.rev[j];
                         if (r >= 0) a.hint_next[r] = (uint8_t)a.stamp_next;
                     }
+                }
             }
+            YSTAMP(5);
             // dense rows: the leaving tiles (lv) always; every position if overflowed (leaving and
             // write-sparse tiles get rows)
             const uint32_t ndense = overflow ? a.ny : a.nt;
@@ -509,38 +542,24 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
             }
             if (nzw) atomicOr(&a.nz_next[v * a.ntw + nz_tw], nzw);
             __builtin_amdgcn_wave_barrier();
+            YSTAMP(6);
             // ---- seen rows materialised from the list: the tiles leaving the young set, or (the
             //      list overflows now) every young position; whole 128-B lines ----
             if (!lovf) {
                 const uint32_t nm = lspill ? a.ny : a.nt;
-                // (1) the new bits of those tiles with their id groups made whole
-                for (uint32_t q0 = 0; q0 < nm; q0 += 4) {
-                    const uint32_t qi = q0 + (lane >> 4), word = lane & 15u;
-                    const uint32_t q = qi >= nm ? 0xffffffffu : lspill ? qi : (uint32_t)s_lv[qi];
-                    if (q < a.nr) {
-                        const uint32_t i = q * 16u + word;
-                        const uint64_t x = s_acc[i];
-                        if (x && (s_wf[i] & WF_GROUP)) {
-                            const uint32_t w = s_yt[q].tile * 16u + word;
-                            s_acc[i] = group_expand(x, a.ctl[w].gmask, a.ctl[w].gstart);
-                        }
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
+                // (1) this tick's new bits stay single bits in the rows (k_births tests an id group
+                //     against seen & ~arrivals: a whole group there would block a same-tick own
+                //     generation that wins over the arrival); the old entries hold whole groups
                 // (2) the old entries of those tiles
-                if (lane < 16u) {
 #pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        const uint32_t idx = lane * 8u + (uint32_t)j;
-                        const uint32_t e = slot_entry(ql, j);
-                        if (idx == 0u || idx > ltot || e == kSlotTomb) continue;
-                        const uint32_t qp = s_ymap[e >> 10];
-                        if (qp >= a.nr) continue;
-                        const bool leaving = (s_yt[qp].flags & (YT_READ | YT_WRITE)) == YT_READ;
-                        if (lspill || leaving)
-                            atomicOr(reinterpret_cast<uint32_t*>(s_acc + qp * 16u + ((e >> 6) & 15u)) + ((e >> 5) & 1u),
-                                     1u << (e & 31u));
-                    }
+                for (uint32_t j = 0; j < 2u; j++) {
+                    const uint32_t e = lentry(j);
+                    const uint32_t qp = e == kSlotTomb ? 0xffu : s_ymap[e >> 10];
+                    if (qp >= a.nr) continue;
+                    const bool leaving = (s_yt[qp].flags & (YT_READ | YT_WRITE)) == YT_READ;
+                    if (lspill || leaving)
+                        atomicOr(reinterpret_cast<uint32_t*>(s_acc + qp * 16u + ((e >> 6) & 15u)) + ((e >> 5) & 1u),
+                                 1u << (e & 31u));
                 }
                 __builtin_amdgcn_wave_barrier();
                 // (3) write the rows (fresh positions: zeros), (4) reset their accumulator words
@@ -581,14 +600,19 @@ __global__ __launch_bounds__(256, 4) void k_pull_young(YoungArgs a) {
             const uint32_t c = wave_sum32(cnt);
             if (lane == 0 && c) {  // no-return atomics: nothing waits on them
                 atomicAdd(&a.recv[v], c);
-                atomicAdd(reinterpret_cast<unsigned long long*>(&a.sent[v]), (unsigned long long)c * a.deg[v]);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&a.sent[v]), (unsigned long long)c * lane_read(dg, jn));
             }
+            YSTAMP(7);
         }
     }
     if (a.snap) {
         snap_local = wave_sum(snap_local);
         if (lane_id == 0 && snap_local) atomicAdd(a.snap, snap_local);
     }
+#ifdef YOUNG_STAMPS
+    if (a.acct && lane_id == 0)
+        for (int k = 0; k < 8; k++) acct_add(a.acct, 20u + (uint32_t)k, (unsigned long long)ycyc[k]);
+#endif
     if (a.acct && lane_id == 0) {
         const uint32_t tv[11] = {t_sl, t_col, t_fb, t_srd, t_swr, t_rw, t_slw, t_miss, t_lr, t_lw, t_mat};
         const uint32_t slot_of[11] = {8, 9, 10, 11, 12, 13, 14, 15, 17, 18, 19};

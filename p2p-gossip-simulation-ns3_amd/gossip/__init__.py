@@ -33,8 +33,6 @@ MODE_DENSE = 2
 F_TRACE = 1
 F_TIMING = 2
 F_NOSKIP = 4
-F_WIDE_PULL = 8
-F_GENERIC_PULL = 16
 F_TILE_PER_TICK = 32
 F_HANDSHAKE = 64
 F_HOP_BATCH = 128

@@ -77,9 +77,10 @@ def test_report_text_matches_oracle(gossip, oracle):
     assert sim.PrintPeriodicStats() == want
 
 
-# Pull kernels: the default choice by window width (lane-shuffle k_pull for narrow windows,
-# scalar-peer k_pull_wide above 64 words), and each kernel forced at every width.
-KERNELS = {"auto": 0, "wide": 8, "generic": 16}
+# Pull variants: the defaults (k_pull over tile lists with saturation bits, dense-row tiles by the
+# layer model), passes over consecutive words (no tile lists: no saturation bits, no dense rows),
+# and dense rows forced on every listed tile.
+KERNELS = {"auto": (), "no_tile_lists": (("pull_tiles", 0),), "dense_rows": (("dense_rows", 1),)}
 
 
 def _trace_parity(gossip, oracle, n, p, seed, sim_time, lat_ms, kind=None, id_mask=0, kflags=0, options=()):
@@ -106,23 +107,23 @@ def _trace_parity(gossip, oracle, n, p, seed, sim_time, lat_ms, kind=None, id_ma
 
 @pytest.mark.parametrize("kern", list(KERNELS))
 def test_trace_parity_sparse_4096(gossip, oracle, kern):
-    _trace_parity(gossip, oracle, 4096, 16.0 / 4095, 21, 6.0, 5.0, kflags=KERNELS[kern])
+    _trace_parity(gossip, oracle, 4096, 16.0 / 4095, 21, 6.0, 5.0, options=KERNELS[kern])
 
 
 @pytest.mark.parametrize("kern", list(KERNELS))
 def test_trace_parity_dense_512(gossip, oracle, kern):
-    _trace_parity(gossip, oracle, 512, 0.3, 22, 8.0, 5.0, kflags=KERNELS[kern])
+    _trace_parity(gossip, oracle, 512, 0.3, 22, 8.0, 5.0, options=KERNELS[kern])
 
 
 @pytest.mark.parametrize("kern", list(KERNELS))
 def test_trace_parity_collisions(gossip, oracle, kern):
     # 0x3FF id mask: dozens of generations per id, id groups of up to ~6 sources
-    _trace_parity(gossip, oracle, 400, 0.01, 23, 15.0, 5.0, id_mask=0x3FF, kflags=KERNELS[kern])
+    _trace_parity(gossip, oracle, 400, 0.01, 23, 15.0, 5.0, id_mask=0x3FF, options=KERNELS[kern])
 
 
 @pytest.mark.parametrize("kern", list(KERNELS))
 def test_trace_parity_odd_latency(gossip, oracle, kern):
-    _trace_parity(gossip, oracle, 300, 0.02, 24, 10.37, 2.3, kflags=KERNELS[kern])
+    _trace_parity(gossip, oracle, 300, 0.02, 24, 10.37, 2.3, options=KERNELS[kern])
 
 
 # Saturation bits and dense-row tiles (pull_kernel.h) against the oracle's counters and traces:
@@ -177,8 +178,8 @@ def test_work_skipping_changes_nothing(gossip, kern):
     topo = gossip.Topology.gnp(n, 10.0 / (n - 1), 41, gossip.TOPO_SKIP)
     t_cut = gossip.seconds_to_ns(8.0)
     ev = gossip.make_schedule(n, 5, T0, t_cut, id_mask=0x3FFF)
-    a = _engine_for(gossip, topo, ev, L, t_cut, flags=KERNELS[kern]).stats()
-    b = _engine_for(gossip, topo, ev, L, t_cut, flags=gossip.F_NOSKIP | KERNELS[kern]).stats()
+    a = _engine_for(gossip, topo, ev, L, t_cut, options=KERNELS[kern]).stats()
+    b = _engine_for(gossip, topo, ev, L, t_cut, flags=gossip.F_NOSKIP, options=KERNELS[kern]).stats()
     for k in STATS:
         assert np.array_equal(getattr(a, k), getattr(b, k)), k
 
@@ -193,11 +194,11 @@ def test_wide_window_kernels_agree(gossip, oracle):
     ev = gossip.make_schedule(n, 7, T0, t_cut)
     a, b = topo.links()
     r = oracle.run_replay(n, L, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
-    runs = [(kern, {}) for kern in KERNELS.values()]
-    runs += [(0, {"pull_nt": 1}), (0, {"pull_nt": 1, "young": 1, "young_nt": 1, "pull_grid": 16384}),
-             (0, {"pull_nt": 1, "dense_rows": 1}), (0, {"pull_nt": 1, "pull_sat": 0, "dense_rows": 0})]
-    for kern, opts in runs:
-        eng = gossip.Engine(n, L, T0, t_cut, flags=kern | gossip.F_TILE_PER_TICK)
+    runs = [dict(o) for o in KERNELS.values()]
+    runs += [{"pull_nt": 1}, {"pull_nt": 1, "young": 1, "young_nt": 1, "pull_grid": 16384},
+             {"pull_nt": 1, "dense_rows": 1}, {"pull_nt": 1, "pull_sat": 0, "dense_rows": 0}]
+    for opts in runs:
+        eng = gossip.Engine(n, L, T0, t_cut, flags=gossip.F_TILE_PER_TICK)
         for k, v in opts.items():
             eng.set_option(k, v)
         eng.set_topology(topo)
@@ -210,7 +211,7 @@ def test_wide_window_kernels_agree(gossip, oracle):
         if opts.get("pull_nt"):
             assert c.pull_nt == 1 and c.pull_lpw == 32, opts  # k_pull<32, 1, true>
         for k in STATS:
-            assert np.array_equal(getattr(st, k), getattr(r, k)), (kern, opts, k)
+            assert np.array_equal(getattr(st, k), getattr(r, k)), (opts, k)
 
 
 def test_tile_list_options_agree(gossip, oracle):
@@ -229,7 +230,7 @@ def test_tile_list_options_agree(gossip, oracle):
     for opts in ({}, {"pull_tile_order": 0}, {"pull_tiles": 0}, prod,
                  dict(prod, young=1, young_nt=1), dict(prod, young=1, young_nt=1, dense_rows=1),
                  dict(prod, dense_rows=1), dict(prod, dense_rows=1, pull_sat=0), {"pull_sat": 0, "dense_rows": 0}):
-        eng = gossip.Engine(n, L, T0, t_cut, flags=gossip.F_TILE_PER_TICK | gossip.F_TRACE | gossip.F_GENERIC_PULL)
+        eng = gossip.Engine(n, L, T0, t_cut, flags=gossip.F_TILE_PER_TICK | gossip.F_TRACE)
         for k, v in opts.items():
             eng.set_option(k, v)
         eng.set_topology(topo)

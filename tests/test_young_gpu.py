@@ -77,14 +77,17 @@ def test_young_seen_lists(gossip, oracle, cap, id_mask):
         assert c.young_seen_reads == 0 and c.young_seen_writes == 0
 
 
-@pytest.mark.parametrize("list_cap,id_mask", [(4, 0x3FF), (12, 0), (127, 0)])
+@pytest.mark.parametrize("list_cap,id_mask", [(4, 0x3FF), (12, 0), (16, 0)])
 def test_young_seen_list_overflow(gossip, oracle, list_cap, id_mask):
     # lists that overflow -- in k_pull_young (more entries than it may keep) and in k_births (a
     # birth, or a whole id group, that does not fit): the node's young seen rows are materialised
     # and it dedups against dense seen words from then on (fresh tiles cleared at that node).
-    # 127: 20,000 nodes, the young set covering every node's 6-hop neighbourhood -- ~170 entries
-    if list_cap == 127:
-        c = _parity(gossip, oracle, 20000, 16.0 / 19999, 83, 5.4, 5.0, dict(young_age=6), trace=False,
+    # (C4's lists hold ~53 entries: none overflows at the default capacity)
+    if list_cap == 16:  # 6,000 nodes, young tiles up to 5 hops: ~23 entries, k_pull_young keeps 8
+        c = _parity(gossip, oracle, 6000, 16.0 / 5999, 83, 5.5, 5.0, dict(young_age=6, young_list_cap=list_cap),
+                    flags=gossip.F_TILE_PER_TICK)
+    elif list_cap == 12:  # (k_pull_young keeps 6 of them: ~11 entries per node here)
+        c = _parity(gossip, oracle, 3000, 12.0 / 2999, 81, 6.0, 5.0, dict(young_age=4, young_list_cap=list_cap),
                     flags=gossip.F_TILE_PER_TICK)
     else:
         c = _parity(gossip, oracle, 400, 0.01, 73, 15.0, 5.0, dict(young_cap=8, young_age=4, young_list_cap=list_cap),
