@@ -331,10 +331,7 @@ __global__ __launch_bounds__(1024) void k_dense_dedup(PullArgs a) {
             }
         }
         const uint32_t c = (uint32_t)wave_sum((unsigned long long)cnt);
-        if (lane == 0 && c) {
-            a.recv[v] += c;
-            a.sent[v] += (uint64_t)c * a.deg[v];
-        }
+        if (lane == 0 && c) a.recv[v] += c;  // (sent: derived, engine.hip)
     }
     if (a.snap) {
         snap_local = wave_sum(snap_local);

@@ -10,6 +10,10 @@
 //   seen[v] |= new[v];  F_{t+1}[v] = new[v] | births  (ReceiveShare inserts + forwards, :155-165)
 //   recv[v] += popcount(new[v]); sent[v] += |peers(v)| * popcount(new[v])
 //
+// sent is stored as the births' sends only (k_births): every reception forwards |peers(v)| copies
+// (p2pnode.cc:163 -> :129-146), so sent = d_sent + deg x recv, formed where sent is read
+// (gossip_engine_get_stats, k_sum_sent) -- the pull kernels then never load a node's |peers|.
+//
 // HBM layout (row-major, node rows): F0, F1, seen are n x stride uint64 words; bit b of word w
 // is share column 64w+b.  A column is one share source; shares whose 32-bit ids collide
 // (GenerateUniqueShareId, p2pnode.cc:201-209, collides above ~128,849 nodes) and that live in
@@ -80,14 +84,13 @@ struct Birth {
 struct PullArgs {
     const int64_t* rowptr;
     const int32_t* col;
-    const uint32_t* deg;
     const uint64_t* Fcur;
     uint64_t* Fnext;
     uint64_t* seen;
     const WordCtl* ctl;     // masks, read only for words whose wflags say so
     const uint8_t* wflags;  // per word: WF_CLEAR | WF_GROUP | WF_KEEP | WF_SNAP
     uint32_t* recv;
-    uint64_t* sent;
+    // (no sent: derived from recv, header comment)
     unsigned long long* live;             // liveness of this tick (OR of F_next words)
     const unsigned long long* live_prev;  // liveness of tick t-1 (nullable: all live)
     unsigned long long* snap;             // nullable
@@ -396,8 +399,7 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
                 } else {
                     if (ovf) *fp &= ~arr;
                     else slot_word_bits(s, hdr, x.widx, w & 15u, arr, true);
-                    a.recv[v] -= 1u;
-                    a.sent[v] -= dv;
+                    a.recv[v] -= 1u;  // (and its deg sends: sent is derived from recv)
                     if (a.snap && aph < a.snap_r) atomicAdd(a.snap, (unsigned long long)-1ll);
                 }
             }
@@ -462,8 +464,7 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
                 // Own generation first (ties: the generation event was scheduled earlier):
                 // the arrival finds the id already processed and is dropped.
                 *fp &= ~arr;
-                a.recv[v] -= 1u;
-                a.sent[v] -= dv;
+                a.recv[v] -= 1u;  // (and its deg sends: sent is derived from recv)
                 if (a.snap && aph < a.snap_r) atomicAdd(a.snap, (unsigned long long)-1ll);
             }
         }
@@ -526,10 +527,12 @@ __global__ __launch_bounds__(256) void k_sum_u32(const uint32_t* a, const uint32
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, s);
 }
 
-__global__ __launch_bounds__(256) void k_sum_u64(const uint64_t* a, uint32_t n,
-                                                 unsigned long long* out) {
+// Σ sent = Σ (births' sends + deg x recv), the derived sent counter (header comment)
+__global__ __launch_bounds__(256) void k_sum_sent(const uint64_t* sb, const uint32_t* recv, const uint32_t* deg,
+                                                  uint32_t n, unsigned long long* out) {
     unsigned long long s = 0;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) s += a[i];
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+        s += sb[i] + (unsigned long long)recv[i] * deg[i];
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, s);
 }
@@ -1922,14 +1925,14 @@ int gossip_engine::tick_step_a(int64_t t) {
     };
     if (wact) {
         PullArgs a;
-        a.rowptr = d_rowptr; a.col = d_col; a.deg = d_deg;
+        a.rowptr = d_rowptr; a.col = d_col;
         if (handshake && t == tick0 + 3) {  // shares sent in [t_start+2L, t_start+3L): a -> b only
             a.rowptr = d_rowptr_c;
             a.col = d_col_c;
         }
         a.Fcur = d_F[fcur]; a.Fnext = d_F[nxt]; a.seen = d_seen; a.ctl = d_ctl[slot];
         a.wflags = d_wflags[slot];
-        a.recv = d_recv; a.sent = d_sent; a.live = d_live[lv]; a.snap = snap_ptr;
+        a.recv = d_recv; a.live = d_live[lv]; a.snap = snap_ptr;
         a.live_prev = (t - 1 >= tick0) ? d_live[(t - 1) % 3] : nullptr;
         a.acct = d_acct;
         a.nz_cur = d_nz[fcur];
@@ -2041,11 +2044,11 @@ int gossip_engine::tick_step_a(int64_t t) {
         }
         auto launch_young = [&](hipStream_t ys) -> int {
             YoungArgs y;
-            y.rowptr = a.rowptr; y.col = a.col; y.deg = d_deg;
+            y.rowptr = a.rowptr; y.col = a.col;
             y.Fcur = d_F[fcur]; y.Fnext = d_F[nxt]; y.seen = d_seen;
             y.slot_cur = d_slot[fcur]; y.slot_next = d_slot[nxt];
             y.ctl = d_ctl[slot]; y.wflags = d_wflags[slot];
-            y.recv = d_recv; y.sent = d_sent; y.live = d_live[lv];
+            y.recv = d_recv; y.live = d_live[lv];
             y.snap = snap_ptr; y.acct = d_acct; y.nz_next = d_nz[nxt]; y.ntw = ntw;
             y.yt = d_young[slot]->yt; y.ny = ny; y.nr = ny_read; y.nt = ny_leave;
             y.lv = d_young[slot]->lv;
@@ -3540,7 +3543,10 @@ int gossip_engine_get_stats(gossip_engine* e, uint32_t* gen, uint32_t* recv, uin
     HIP_TRY(hipMemcpy(r.data(), e->d_recv, n * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(g.data(), e->d_gen, n * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(eg.data(), e->d_effgen, n * 4, hipMemcpyDeviceToHost));
-    if (sent) HIP_TRY(hipMemcpy(sent, e->d_sent, n * 8, hipMemcpyDeviceToHost));
+    if (sent) {  // births' sends + deg x recv (header comment)
+        HIP_TRY(hipMemcpy(sent, e->d_sent, n * 8, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n; i++) sent[i] += (uint64_t)r[i] * e->h_peers[i];
+    }
     if (gen) std::memcpy(gen, g.data(), n * 4);
     if (recv) std::memcpy(recv, r.data(), n * 4);
     if (fwd) std::memcpy(fwd, r.data(), n * 4);  // sharesForwarded++ beside sharesReceived++
@@ -3610,7 +3616,7 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     e->pull_ms_done = ms;
     c->pull_ms = ms;
     HIP_TRY(hipMemsetAsync(e->d_scalars, 0, 16, e->stream));
-    k_sum_u64<<<256, 256, 0, e->stream>>>(e->d_sent, e->n, e->d_scalars);
+    k_sum_sent<<<256, 256, 0, e->stream>>>(e->d_sent, e->d_recv, e->d_deg, e->n, e->d_scalars);
     k_sum_u32<<<256, 256, 0, e->stream>>>(e->d_recv, nullptr, e->n, e->d_scalars + 1);
     HIP_TRY(hipGetLastError());
     unsigned long long v[2];

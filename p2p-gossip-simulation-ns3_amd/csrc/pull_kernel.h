@@ -4,7 +4,8 @@
 // One tick of P2PNode::HandleRead -> processedShares check -> ReceiveShare ->
 // GossipShareToPeers (p2pnode.cc:127-199) for every node at once:
 //     inc = OR_{u in peers(v)} F_cur[u];  new = inc & ~seen[v] & keep;  seen |= new;
-//     F_next[v] = new;  recv[v] += popcount(new);  sent[v] += |peers(v)| * popcount(new)
+//     F_next[v] = new;  recv[v] += popcount(new)   (sent[v] += |peers(v)| * popcount(new) is
+//     derived: engine.hip, sent = births' sends + deg x recv)
 //
 // Lane layout: a node is served by GRP = LPW x EPN lanes.  Word-lane wl owns the 16-B word pair
 // [2wl, 2wl+1] of every 2*LPW-word pass; edge-lane el takes every EPN-th peer.  Wide windows
@@ -255,10 +256,6 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
         PULL_LANES
         const int64_t rp = a.rowptr[min(c0 + lane, n)];
         const int64_t rp_end = a.rowptr[min(c0 + 64u, n)];
-        // |peers| with multiplicity of the chunk's node `lane` (sent += new x deg): loaded with the
-        // row pointers -- a load after a node's stores waits for all of them (vmcnt(0)), and
-        // would drain the item pipeline's prefetches once per node
-        const uint32_t dg = a.deg[min(c0 + lane, n - 1u)];
         if (sat_on) {  // the chunk's sat words, trusted bits only (waited for below)
 #pragma unroll
             for (uint32_t q = 0; q < 2u; q++) {
@@ -581,15 +578,13 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
                 }
             }
             // ---- per-node counters after the node's last pass ----
-            // (no-return atomics: nothing waits on them -- a read-modify-write would load, and
-            // that wait drains every prefetch and store in flight)
+            // (a no-return atomic: nothing waits on it -- a read-modify-write, or a load of the
+            // node's |peers| here, would wait with the item's stores outstanding, vmcnt(0), and
+            // drain the pipeline's prefetches once per node.  sent is not touched: every reception
+            // sends |peers| copies, so the engine derives sent = births' sends + deg x recv)
             if (pass + 1u == npass) {
                 const uint32_t c = group_add<GRP>(cnt, lane);
-                const uint32_t dv = lane_get(dg, idx);  // (whole wave active)
-                if (gl == 0 && c) {
-                    atomicAdd(&a.recv[v], c);
-                    atomicAdd(reinterpret_cast<unsigned long long*>(&a.sent[v]), (unsigned long long)c * dv);
-                }
+                if (gl == 0 && c) atomicAdd(&a.recv[v], c);
                 cnt = 0;
             }
             // ---- advance the pipeline ----

@@ -83,7 +83,6 @@ struct YoungTile {
 struct YoungArgs {
     const int64_t* rowptr;
     const int32_t* col;
-    const uint32_t* deg;
     const uint64_t* Fcur;
     uint64_t* Fnext;
     uint64_t* seen;
@@ -92,7 +91,6 @@ struct YoungArgs {
     const WordCtl* ctl;
     const uint8_t* wflags;
     uint32_t* recv;
-    uint64_t* sent;
     unsigned long long* live;
     unsigned long long* snap;  // nullable
     unsigned long long* acct;  // nullable
@@ -224,9 +222,6 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
         const uint32_t cnt_nodes = (uint32_t)min<uint64_t>(64u, a.n - c0);
         const int64_t rp = a.rowptr[c0 + min(lane, cnt_nodes)];
         const int64_t rp_end = a.rowptr[c0 + cnt_nodes];
-        // |peers| with multiplicity of node j in lane j (sent += c x deg): loaded with the row
-        // pointers, not after the node's stores (a load there waits for all of them, vmcnt(0))
-        const uint32_t dg = a.deg[c0 + min(lane, cnt_nodes - 1u)];
         // peer ids of node j (lane p = peer p of its first 64), one node ahead of the gather
         // (the peer's id and its hint byte, combined only when the node's gather starts: bit 31
         // of the id says the peer's slot has a second line -- ids are < 2^31)
@@ -598,10 +593,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
                     t_mat += wave_count(qq < a.ny && (lane & 15u) == 0u);
                 }
             const uint32_t c = wave_sum32(cnt);
-            if (lane == 0 && c) {  // no-return atomics: nothing waits on them
-                atomicAdd(&a.recv[v], c);
-                atomicAdd(reinterpret_cast<unsigned long long*>(&a.sent[v]), (unsigned long long)c * lane_read(dg, jn));
-            }
+            if (lane == 0 && c) atomicAdd(&a.recv[v], c);  // no-return: nothing waits (sent: derived)
             YSTAMP(7);
         }
     }

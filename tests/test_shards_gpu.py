@@ -49,7 +49,8 @@ T0 = 5_000_000_000
 
 def _burst(gossip):
     """4,096 distinct shares born in one tick of a 20,000-node sparse graph: a 96-word window
-    (~46 MB) for one engine, 64 words (~31 MB) for each of 2 shards."""
+    (48.5 MB of bitmaps, graph, counters, occupancy and saturation words) for one engine, 80 words
+    (40.8 MB) for each of 2 shards -- so a 44 MB budget takes exactly 2 (tools/diag/shard_fallback.py)."""
     rng = np.random.Generator(np.random.Philox(11))
     nodes = rng.choice(N_BURST, size=4096, replace=False)
     return gossip.events_from_arrays(T0 + 1000 + np.arange(4096, dtype=np.int64), nodes,
@@ -63,7 +64,7 @@ def test_cli_falls_back_to_more_shards(gossip, tmp_path):
     base = [f"--numNodes={N_BURST}", f"--connectionProb={16.0 / (N_BURST - 1)}", "--simTime=5.3",
             "--seed=8", f"--events={evf}", "--quiet"]
     one = _sim(*base)
-    lim = _sim(*base, "--memLimitMB=40")
+    lim = _sim(*base, "--memLimitMB=44")
     assert "retrying with 2" in lim.stderr
     assert "engines: 2 share shards" in lim.stdout
     assert _report(lim.stdout) == _report(one.stdout)
@@ -71,7 +72,7 @@ def test_cli_falls_back_to_more_shards(gossip, tmp_path):
 
 def test_simulation_falls_back_to_more_shards(gossip, oracle):
     ev = _burst(gossip)
-    sim = gossip.P2PGossipNetworkSimulation(N_BURST, topo_seed=8, options={"mem_limit": 40 << 20})
+    sim = gossip.P2PGossipNetworkSimulation(N_BURST, topo_seed=8, options={"mem_limit": 44 << 20})
     sim.CreateRandomTopology(16.0 / (N_BURST - 1), 5.0)
     st = sim.Start(5.3, events=ev)
     assert sim.shards_used == 2
