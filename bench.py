@@ -190,7 +190,10 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
         acc["pull_tiles"] = c1.pull_tiles
         acc["lpw"], acc["pull_sat"] = c1.pull_lpw, c1.pull_sat
         acc["dense_tiles"] = max(acc.get("dense_tiles", 0), c1.pull_dense_tiles)
-        acc["sat_skips"] = acc.get("sat_skips", 0) + c1.pull_sat_skips - c0.pull_sat_skips
+        # (device-side tallies restart at reset_timing: c1 holds the timed ticks alone)
+        acc["sat_skips"] = acc.get("sat_skips", 0) + c1.pull_sat_skips
+        acc["items"] = acc.get("items", 0) + c1.pull_items
+        acc["gather_items"] = acc.get("gather_items", 0) + c1.pull_gather_items
         acc["early_retires"] = acc.get("early_retires", 0) + c1.window_early_retires
         acc["ramp_ticks"] = c0.ticks
         if rank == 0:
@@ -444,6 +447,8 @@ def main():
                     16 * (acc["srd"] + acc["swr"] + acc["fwr"])),
             },
             "saturated_tiles_skipped_per_launch": per_launch(acc.get("sat_skips", 0)),
+            "items_per_launch": per_launch(acc.get("items", 0)),
+            "gather_items_per_launch": per_launch(acc.get("gather_items", 0)),
             "dense_row_tiles_last_tick": acc.get("dense_tiles", 0),
         }
         variant = {"nt_rows": acc["nt"], "grid": acc["grid"],

@@ -387,6 +387,8 @@ typedef struct gossip_counters {
     uint64_t window_early_retires; /* allocations that first retired tiles from the last tick's
                                       liveness (the window near its capacity) since creation */
     uint64_t young_list_lines;   /* seen-list lines k_pull_young read and wrote [128 B] since reset */
+    uint64_t pull_items;         /* k_pull work items (node, pass) since reset */
+    uint64_t pull_gather_items;  /* of those, items that gathered some peer row since reset */
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 /* Option rehearse_rows = R: per row block r < R, summed since the last reset_timing -- pull time,

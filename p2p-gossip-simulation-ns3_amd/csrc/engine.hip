@@ -3698,6 +3698,8 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     c->pull_lpw = e->last_lpw;
     c->pull_dense_tiles = e->last_dense_tiles;
     c->pull_sat_skips = acct[16];
+    c->pull_items = acct[20];
+    c->pull_gather_items = acct[21];
     c->pull_sat = e->sat_used ? 1u : 0u;
     c->window_early_retires = e->early_retires;
     uint64_t g = 0;

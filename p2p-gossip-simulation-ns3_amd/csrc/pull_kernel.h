@@ -147,8 +147,10 @@ __host__ __device__ constexpr size_t pull_lds_bytes(uint32_t wact, bool keep = f
            (((size_t)nptile * 2u + 15u) & ~(size_t)15u);
 }
 // + (option pull_sat) the launch's two occupancy words of tmask and every wave's sat words of its
-// 64 nodes (2 per node), behind the rest
-constexpr size_t kPullSatLds = 8u * 8u + 4u * 64u * 2u * 8u;
+// 64 nodes (2 per node), the passes' live-tile masks and forced passes, every wave's per-step pass
+// masks (empty items skipped), behind the rest
+constexpr uint32_t kPullMaxPasses = 32;  // passes of a listed launch: kPullLdsWords / 16 / 4 tiles
+constexpr size_t kPullSatLds = 8u * 8u + 4u * 64u * 2u * 8u + kPullMaxPasses * 8u + 16u + 4u * kPullMaxPasses * 4u;
 static_assert(2u * TM_WORDS <= 8u, "tmask words of a launch fit their LDS slot");
 constexpr uint32_t kNoWord = 0xffffffffu;
 
@@ -192,9 +194,45 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
     unsigned long long* s_tm = reinterpret_cast<unsigned long long*>(
         reinterpret_cast<char*>(smem) + pull_lds_bytes(a.wact, a.keep_lds != 0, a.nptile));
     unsigned long long* s_sat = s_tm + 8;  // [wave][node of the chunk][occupancy word of the launch]
+    unsigned long long* s_plm = s_sat + 4u * 128u;  // [pass] live tiles (bits by tile in its nz word)
+    uint32_t* s_pforce = reinterpret_cast<uint32_t*>(s_plm + kPullMaxPasses);  // passes every node runs
+    uint32_t* s_smask = s_pforce + 4;  // [wave][step] passes some node of the step has work in
     if (threadIdx.x < 2u * TM_WORDS) {
         const uint32_t twg = (a.wbase >> 10) + threadIdx.x / TM_WORDS;
         s_tm[threadIdx.x] = (tm_on && twg < a.ntw) ? a.tmask[twg * TM_WORDS + threadIdx.x % TM_WORDS] : 0ull;
+    }
+    // Empty items (tile lists with tmask): an item (node, pass) whose every tile is saturated at
+    // the node (a trusted sat bit) or dead (no live column) moves nothing and changes nothing, so
+    // the item sequence skips it.  Passes holding a tile that must be written or cleared anyway
+    // (WF_CLEAR, WF_DW, WF_KEEP) and the last pass of each occupancy word (the node's nz and sat
+    // words are written back there, its counters after the last pass) are never skipped.
+    constexpr uint32_t TPP_ = LPW >= 8 ? (uint32_t)LPW / 8u : 1u;
+    const bool skip_on = tm_on && a.nptile / TPP_ <= kPullMaxPasses;
+    __syncthreads();  // (s_lp, s_wf, s_pt written)
+    if (skip_on && threadIdx.x < 64u) {
+        const uint32_t p = threadIdx.x, np = a.nptile / TPP_;
+        unsigned long long lm = 0ull;
+        bool force = p + 1u == np;
+        if (p < np) {
+            for (uint32_t k = 0; k < TPP_; k++) {
+                const uint32_t t = s_pt[p * TPP_ + k];
+                if (t == 0xffffu) continue;
+                unsigned long long lv = 0ull;
+                uint32_t fl = 0u;
+                for (uint32_t q = 0; q < 16u; q++) {
+                    lv |= s_lp[t * 16u + q];
+                    fl |= s_wf[t * 16u + q];
+                }
+                if (lv) lm |= 1ull << (((a.wbase >> 4) + t) & 63u);
+                if (fl & (WF_CLEAR | WF_DW | WF_KEEP)) force = true;
+            }
+            if (p + 1u < np && ((a.wbase + (uint32_t)s_pt[(p + 1u) * TPP_] * 16u) >> 10) !=
+                                   ((a.wbase + (uint32_t)s_pt[p * TPP_] * 16u) >> 10))
+                force = true;
+            s_plm[p] = lm;
+        }
+        const unsigned long long fm = __ballot(p < np && force);
+        if (threadIdx.x == 0) s_pforce[0] = (uint32_t)fm;
     }
     __syncthreads();
     const uint32_t lane_id = threadIdx.x & 63u;
@@ -238,6 +276,7 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
     const uint32_t nsteps = 64u / NPW;
     unsigned long long snap_local = 0ull;
     uint32_t t_pe = 0, t_col = 0, t_srd = 0, t_swr = 0, t_fwr = 0, t_nz = 0, t_sk = 0;  // wave-uniform
+    uint32_t t_it = 0, t_gi = 0;  // node items, node items that gathered
     unsigned long long nzacc = 0ull;
     const bool gather = EPN == 1;  // the pipelined id/occupancy loads
     const uint32_t tw_base = a.wbase >> 10;  // the launch's first occupancy word
@@ -265,23 +304,58 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
                                             ? a.sat[vj * a.ntw + twg] & s_tm[q * TM_WORDS + TM_SATOK] : 0ull;
             }
         }
+        // per step, the passes some node of the step has work in (skip_on; else every pass)
+        uint32_t* s_sm = s_smask + wave_in_block() * kPullMaxPasses;
+        if (skip_on) {
+            uint32_t m = s_pforce[0];
+            const uint64_t vj = c0 + lane;
+            if (vj < n) {
+                for (uint32_t p = 0; p < npass; p++) {
+                    const uint32_t twp = tw_of(p) - tw_base;
+                    // (s_satw: this lane's node, written above by this lane)
+                    if ((s_plm[p] & ~(sat_on ? s_satw[lane * 2u + twp] : 0ull)) != 0ull) m |= 1u << p;
+                }
+            }
+            m = group_or<NPW>(m, lane);  // (the NPW nodes of a step are adjacent lanes)
+            if (lane % NPW == 0u) s_sm[lane / NPW] = m;
+            __builtin_amdgcn_wave_barrier();
+        }
+        // the item after (step, pass): the step's next pass with work, else the next step's first
+        auto next_item = [&](uint32_t st, uint32_t ps, uint32_t& st1, uint32_t& ps1) {
+            if (!skip_on) {
+                st1 = ps + 1u < npass ? st : st + 1u;
+                ps1 = ps + 1u < npass ? ps + 1u : 0u;
+                return;
+            }
+            const uint32_t m = ps + 1u < 32u ? s_sm[st] & ~((2u << ps) - 1u) : 0u;
+            if (m) {
+                st1 = st;
+                ps1 = (uint32_t)__builtin_ctz(m);
+            } else {
+                st1 = st + 1u;
+                ps1 = st1 < nsteps ? (uint32_t)__builtin_ctz(s_sm[st1]) : 0u;
+            }
+        };
         // item k = (step, pass): node c0 + step * NPW + slot, the lane's word pair lw_of(pass)
-        uint32_t step = 0, pass = 0;
+        uint32_t step = 0, pass = skip_on ? (uint32_t)__builtin_ctz(s_sm[0]) : 0u;
+        uint32_t first_step = 0xffffffffu;  // the step whose peer range beg/end holds
         ulonglong2 s2c = make_ulonglong2(0ull, 0ull);
         {
             const uint64_t v = c0 + slot;
-            const uint32_t lw = lw_of(0u, wl);
+            const uint32_t lw = lw_of(pass, wl);
             if (v < n && lw != kNoWord && (s_lp[lw] | s_lp[lw + 1u]) != 0ull &&
-                !((satv_of(slot, tw_of(0u)) >> (((a.wbase + lw) >> 4) & 63u)) & 1ull))
+                !((satv_of(slot, tw_of(pass)) >> (((a.wbase + lw) >> 4) & 63u)) & 1ull))
                 s2c = load_row16<NT>(a.seen + v * stride + a.wbase + lw);
         }
         uint32_t cid0 = 0xffffffffu, cid1 = 0xffffffffu;
         unsigned long long nz0 = 0ull;
         if (gather) {
+            uint32_t s1, p1;
+            next_item(0u, pass, s1, p1);
             cid0 = pull_cid_load<LPW, EPN>(a, 0u, c0, rp, rp_end, gl, slot);
-            cid1 = npass > 1u ? cid0 : pull_cid_load<LPW, EPN>(a, 1u, c0, rp, rp_end, gl, slot);
-            const bool ld = cid0 != 0xffffffffu && nz_needed(slot, tw_of(0u));
-            nz0 = ld ? a.nz_cur[(uint64_t)cid0 * a.ntw + tw_of(0u)] : 0ull;
+            cid1 = s1 == 0u ? cid0 : pull_cid_load<LPW, EPN>(a, s1, c0, rp, rp_end, gl, slot);
+            const bool ld = cid0 != 0xffffffffu && nz_needed(slot, tw_of(pass));
+            nz0 = ld ? a.nz_cur[(uint64_t)cid0 * a.ntw + tw_of(pass)] : 0ull;
             t_nz += wave_count(ld);
         }
         uint32_t cnt = 0;
@@ -301,15 +375,20 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
         while (step < nsteps) {
             PULL_LANES
             // ---- geometry of this item and the next two ----
-            const uint32_t step1 = pass + 1u < npass ? step : step + 1u;
-            const uint32_t pass1 = pass + 1u < npass ? pass + 1u : 0u;
-            const uint32_t step2 = pass1 + 1u < npass ? step1 : step1 + 1u;
+            uint32_t step1, pass1, step2, pass2;
+            next_item(step, pass, step1, pass1);
+            if (step1 < nsteps)
+                next_item(step1, pass1, step2, pass2);
+            else
+                step2 = nsteps;
+            (void)pass2;
             const uint32_t idx = step * NPW + slot;
             const uint32_t v = (uint32_t)(c0 + idx);
             const uint32_t lw0 = lw_of(pass, wl);
             const uint32_t w = a.wbase + (lw0 == kNoWord ? 0u : lw0);
             const bool act = c0 + idx < n && lw0 != kNoWord;
-            if (pass == 0u) {  // (uniform) a new node: its peer range, with the whole wave active
+            if (step != first_step) {  // (uniform) a new node: its peer range, with the whole wave active
+                first_step = step;
                 beg = (int32_t)lane_get((uint32_t)rp, idx);
                 const int32_t nxb = (int32_t)lane_get((uint32_t)rp, (idx + 1u) & 63u);
                 end = (idx + 1u < 64u) ? nxb : (int32_t)rp_end;
@@ -400,6 +479,8 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
             const bool tneed = tn != 0 && act;
             int gneed = tn;
             gneed = (int)group_or<GRP>((uint32_t)gneed, lane);
+            t_it += wave_count(gl == 0 && c0 + idx < n);
+            t_gi += wave_count(gl == 0 && gneed != 0);
             // ---- gather peer rows ----
             uint64_t acc0 = 0ull, acc1 = 0ull;
             if (gneed) {  // uniform inside the node group
@@ -603,10 +684,10 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
         if (lane_id == 0 && snap_local) atomicAdd(a.snap, snap_local);
     }
     if (a.acct && lane_id == 0) {
-        const uint32_t tv[7] = {t_pe, t_col, t_srd, t_swr, t_fwr, t_nz, t_sk};
-        const int slot_of[7] = {0, 1, 2, 3, 4, 7, 16};
+        const uint32_t tv[9] = {t_pe, t_col, t_srd, t_swr, t_fwr, t_nz, t_sk, t_it, t_gi};
+        const int slot_of[9] = {0, 1, 2, 3, 4, 7, 16, 20, 21};
 #pragma unroll
-        for (int q = 0; q < 7; q++)
+        for (int q = 0; q < 9; q++)
             if (tv[q]) acct_add(a.acct, (uint32_t)slot_of[q], (unsigned long long)tv[q]);
     }
     __syncthreads();

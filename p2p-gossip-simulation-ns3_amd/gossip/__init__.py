@@ -111,6 +111,7 @@ class gossip_counters(C.Structure):
         ("pull_lpw", C.c_uint32), ("pull_dense_tiles", C.c_uint32),
         ("pull_sat_skips", C.c_uint64), ("pull_sat", C.c_uint32), ("pad0", C.c_uint32),
         ("window_early_retires", C.c_uint64), ("young_list_lines", C.c_uint64),
+        ("pull_items", C.c_uint64), ("pull_gather_items", C.c_uint64),
     ]
 
 

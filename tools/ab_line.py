@@ -14,7 +14,8 @@ for k, v in ks.items():
     if "peer_rows" in br:
         parts.append(f"peer_rows {br['peer_rows'] / 1e9:.1f} GB occ {br['peer_occupancy'] / 1e9:.2f} GB "
                      f"seen_rd {br['own_seen_read'] / 1e9:.1f} GB sat_skips {v.get('saturated_tiles_skipped_per_launch', 0) / 1e6:.1f}M "
-                     f"dense_tiles {v.get('dense_row_tiles_last_tick', 0)}")
+                     f"dense_tiles {v.get('dense_row_tiles_last_tick', 0)} "
+                     f"items {v.get('items_per_launch', 0) / 1e6:.1f}M gather {v.get('gather_items_per_launch', 0) / 1e6:.1f}M")
 c = d["config"]
 parts.append(f"words {c['live_words_per_node']}/{c['window_capacity_words']} early {c.get('window_early_retires')} "
              f"shards {c['share_shards']} retried {c.get('shards_retried')}")
