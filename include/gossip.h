@@ -263,6 +263,8 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *   "pull_nt"          -1 auto (non-temporal rows when the live frontier n x wact x 8 B exceeds
  *                      16 GiB), 0 / 1 forced                              [GOSSIP_PULL_NT]
  *   "pull_grid"        blocks per pull launch, 0 = auto (16,384 non-temporal, else 4,096)
+ *   "pull_lds_min"     LDS bytes every k_pull block reserves at least (0 = what it uses): caps
+ *                      k_pull's blocks per CU so that k_pull_young blocks fit beside them
  *                                                                         [GOSSIP_PULL_GRID]
  *   "pull_tile_order"  1: k_pull's tile lists in age order inside each occupancy word (default),
  *                      0: in tile order                                [GOSSIP_PULL_TILE_ORDER]

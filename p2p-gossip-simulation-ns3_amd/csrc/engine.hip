@@ -682,6 +682,8 @@ struct gossip_engine {
     // ---- tuning options (gossip_engine_set_option; environment defaults)
     int64_t opt_pull_nt = -1;         // -1 = by live footprint (kPullNtBytes), 0/1 forced
     int64_t opt_pull_grid = 0;        // 0 = pull_grid_cap's default
+    int64_t opt_pull_lds_min = 0;     // k_pull launches reserve at least this much LDS per block
+                                      // (caps its blocks per CU, leaving CUs room for k_pull_young)
     int64_t opt_pull_lpw = 0;         // 0 = 32 word-lanes for wide windows
     int64_t opt_dense_min_tiles = 512;  // block tiles the MFMA K split aims for
     int64_t opt_young = -1;           // young tiles (k_pull_young): -1 auto, 0 off, 1 on
@@ -1985,8 +1987,9 @@ int gossip_engine::tick_step_a(int64_t t) {
                     sat_launches += sat_used;
                 }
                 last_lpw = (uint32_t)lpw;
-                launch_pull(lpw, epn, nt_rows, grid, pull_lds_bytes(c.wact, c.keep_lds != 0, c.nptile) + extra_lds,
-                            stream, c);
+                const size_t lds = std::max<size_t>(pull_lds_bytes(c.wact, c.keep_lds != 0, c.nptile) + extra_lds,
+                                                    (size_t)opt_pull_lds_min);
+                launch_pull(lpw, epn, nt_rows, grid, lds, stream, c);
             }
         };
         hipEvent_t e0 = nullptr, e1 = nullptr, p0 = nullptr, p1 = nullptr;
@@ -2857,6 +2860,7 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->cur = e->tick0;
         e->opt_pull_nt = env_option("GOSSIP_PULL_NT", -1);
         e->opt_pull_grid = env_option("GOSSIP_PULL_GRID", 0);
+        e->opt_pull_lds_min = env_option("GOSSIP_PULL_LDS_MIN", 0);
         e->opt_pull_lpw = env_option("GOSSIP_PULL_LPW", 0);
         e->opt_dense_min_tiles = env_option("GOSSIP_DENSE_MIN_TILES", 512);
         e->opt_young = env_option("GOSSIP_YOUNG", -1);
@@ -3173,6 +3177,9 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     if (k == "pull_nt") {
         if (value < -1 || value > 1) return set_error(GOSSIP_EINVAL, "pull_nt: -1 (auto), 0 or 1");
         e->opt_pull_nt = value;
+    } else if (k == "pull_lds_min") {
+        if (value < 0 || value > 160 * 1024) return set_error(GOSSIP_EINVAL, "pull_lds_min: 0 .. 163840 bytes");
+        e->opt_pull_lds_min = value;
     } else if (k == "pull_grid") {
         if (value < 0 || value > (1ll << 24)) return set_error(GOSSIP_EINVAL, "pull_grid: 0 (auto) .. 2^24 blocks");
         e->opt_pull_grid = value;
