@@ -157,8 +157,9 @@ __device__ __forceinline__ uint32_t slot_entry(const ulonglong2& q, int j) {
     return (uint32_t)(word >> (16 * (j & 3))) & 0xffffu;
 }
 
-__device__ __forceinline__ uint32_t lanes_below(unsigned long long m, uint32_t lane) {
-    return (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+// Set bits of m below the calling lane (v_mbcnt: 2 VALU, no 64-bit shift of a lane mask).
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 // Diagnostic build YOUNG_STAMPS: shader cycles per phase of the node loop (s_memtime), summed
@@ -170,6 +171,8 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m, uint32_t l
         ycyc[k] += ys_t - ylast;                               \
         ylast = ys_t;                                          \
     } while (0)
+#elif defined(YOUNG_MARKS)
+#define YSTAMP(k) asm volatile(";YMARK " #k ::)
 #else
 #define YSTAMP(k) \
     do {          \
@@ -247,14 +250,16 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             const uint32_t lane = opaque(lane_id);
             const uint64_t v = c0 + jn;
             // the 8 entries of a lane's 16-B piece of a slot line; `hdr`: entry 0 is the line's header
-            const uint32_t spare = nrw + (lane & (kYoungSpare - 1u));
+            const uint32_t spare_h = 2u * (nrw + (lane & (kYoungSpare - 1u)));  // (half-word index)
             auto scatter8 = [&](const ulonglong2& q, bool hdr) {
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
                     const uint32_t e = (j == 0 && hdr) ? kSlotTomb : slot_entry(q, j);
-                    // (w >= nrw lands in [nrw, spare] -- the spare words).  32-bit LDS atomics on
-                    // the half word holding the bit: half the data moved per lane, one mask register
-                    atomicOr(reinterpret_cast<uint32_t*>(s_acc + min(e >> 6, spare)) + ((e >> 5) & 1u), 1u << (e & 31u));
+                    // 32-bit LDS atomics on the half word holding the bit, e >> 5 (half the data moved
+                    // per lane, one mask register); a tombstone's half word (> every real one) is
+                    // clamped into the lane's spare word.  4 VALU per entry: extract, clamp,
+                    // address, mask
+                    atomicOr(reinterpret_cast<uint32_t*>(s_acc) + min(e >> 5, spare_h), 1u << (e & 31u));
                 }
             };
             const int32_t beg = (int32_t)lane_read((uint32_t)rp, jn);
@@ -413,7 +418,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
                 const uint32_t i = i0 + lane;
                 const bool hit = i < nrw && s_acc[i] != 0ull;
                 const unsigned long long m = __ballot(hit);
-                if (hit) s_list[ntouch + lanes_below(m, lane)] = (uint16_t)i;
+                if (hit) s_list[ntouch + lanes_below(m)] = (uint16_t)i;
                 ntouch += (uint32_t)__popcll(m);
             }
             __builtin_amdgcn_wave_barrier();
