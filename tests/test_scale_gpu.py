@@ -207,7 +207,7 @@ def test_c4_headline_kernels_match_oracle_b(gossip, oracle, c4):
     # ORACLE B (p2pnode.cc:127-199).  A fresh tile per tick (F_TILE_PER_TICK) gives the window of ~25
     # tiles those kernels need at a CPU-checkable 480 generations; young tiles and NT rows are forced
     # (auto keys them off the slice's full ~14k births per tick); dense rows are forced on every
-    # listed tile (auto: a 20-share tile's rows are not dense) and off.
+    # listed tile (auto: a 20-share tile's rows are not dense).
     W = _w()
     topo = c4[0]
     n = topo.num_nodes
@@ -217,10 +217,10 @@ def test_c4_headline_kernels_match_oracle_b(gossip, oracle, c4):
     del a, b
     assert ref.edge_events > 1e10
     prod = (("young", 1), ("young_nt", 1), ("pull_nt", 1), ("pull_grid", 16384), ("pull_tile_order", 1))
+    # (saturation bits and dense rows off: tests/test_engine_gpu.py's option variants, small graphs)
     variants = [
         ("production kernels, dense rows auto", prod),
         ("production kernels, dense rows on every listed tile", prod + (("dense_rows", 1),)),
-        ("production kernels, no saturation bits, no dense rows", prod + (("pull_sat", 0), ("dense_rows", 0))),
     ]
     for name, opts in variants:
         st, c = _run(gossip, topo, ev, W.T0_NS, t_cut, options=opts, flags=gossip.F_TILE_PER_TICK)
