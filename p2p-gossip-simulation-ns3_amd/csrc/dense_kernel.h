@@ -63,7 +63,10 @@ __global__ __launch_bounds__(256) void k_transpose(const uint64_t* __restrict__ 
                                                    uint32_t n, uint32_t kw, uint32_t nwords,
                                                    const unsigned long long* live_prev,
                                                    const unsigned long long* __restrict__ nz,
-                                                   uint32_t ntw, uint32_t* __restrict__ FT) {
+                                                   uint32_t ntw, uint32_t* __restrict__ FT,
+                                                   unsigned long long* phase_ts) {
+    // the DENSE phase's start: the earliest block's start time (engine.hip, k_phase_acc)
+    if (phase_ts && threadIdx.x == 0) atomicMin(phase_ts, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t chunk = blockIdx.x * 4u + wave_in_block();  // 64-node chunk
     const uint32_t w = blockIdx.y;
@@ -349,5 +352,9 @@ __global__ __launch_bounds__(1024) void k_dense_dedup(PullArgs a) {
         if (!x) continue;
         const unsigned long long have = __hip_atomic_load(&a.live[a.wbase + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (x & ~have) atomicOr(&a.live[a.wbase + i], x);
+    }
+    if (a.phase_ts) {  // the DENSE phase's end: the latest block's end time (engine.hip, k_phase_acc)
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(a.phase_ts + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
 }

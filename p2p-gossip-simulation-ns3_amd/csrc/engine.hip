@@ -112,6 +112,8 @@ struct PullArgs {
     // counters are added and occupancy bits OR'ed atomically (nz_next zeroed beforehand)
     uint32_t shared_out = 0;
     uint32_t keep_lds = 0;  // some word of the launch has WF_KEEP: masks staged in LDS (k_pull)
+    // DENSE phase span (k_dense_dedup): every block ORs its end time (s_memrealtime) into [1]
+    unsigned long long* phase_ts = nullptr;
     uint32_t gate_seen = 1;  // k_pull<LPW,1>: skip the own-seen loads of tiles no peer occupies
     // Pass -> tile map (option pull_tiles): a k_pull pass covers LPW / 8 tiles taken from this
     // list of launch-local tile indices (0xffff = padding) instead of LPW / 8 consecutive tiles,
@@ -527,6 +529,14 @@ __global__ __launch_bounds__(256) void k_sum_u32(const uint32_t* a, const uint32
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, s);
 }
 
+// One tick's DENSE phase span into ts[2] (ts[3] counts them); resets the start / end stamps.
+__global__ void k_phase_acc(unsigned long long* ts) {
+    if (ts[1] > ts[0] && ts[0] != ~0ull) ts[2] += ts[1] - ts[0];
+    ts[3] += 1ull;
+    ts[0] = ~0ull;
+    ts[1] = 0ull;
+}
+
 // Σ sent = Σ (births' sends + deg x recv), the derived sent counter (header comment)
 __global__ __launch_bounds__(256) void k_sum_sent(const uint64_t* sb, const uint32_t* recv, const uint32_t* deg,
                                                   uint32_t n, unsigned long long* out) {
@@ -660,6 +670,7 @@ struct gossip_engine {
     unsigned long long* d_inc = nullptr;  // n x stride incoming words (GEMM -> pull)
     uint32_t *d_recv = nullptr, *d_gen = nullptr, *d_effgen = nullptr;
     uint64_t* d_sent = nullptr;
+    unsigned long long* d_phase_ts = nullptr;  // DENSE phase span: [0] start (min), [1] end (max), [2] sum of spans
     unsigned long long* d_live[3] = {nullptr, nullptr, nullptr};  // liveness ring (tick % 3)
     unsigned long long* d_scalars = nullptr;  // [0]=scratch, [1..]=snapshot base/partial
     unsigned long long* d_acct = nullptr;     // k_pull traffic accounting (since reset)
@@ -859,7 +870,7 @@ gossip_engine::~gossip_engine() {
     hipFree(d_rowptr_c); hipFree(d_col_c); hipFree(d_degc);
     for (int k = 0; k < 4; k++) { hipFree(d_smask[k]); hipHostFree(h_smask[k]); }
     hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen_mem); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_sat); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
-    hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent);
+    hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent); hipFree(d_phase_ts);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     hipFree(d_msg); hipFree(d_cnt); hipFree(d_scan_tmp); hipFree(d_recv_msgs); hipFree(d_sizes);
     hipFree(d_tot); hipFree(d_ovf); hipHostFree(h_tot);
@@ -1179,6 +1190,11 @@ int gossip_engine::alloc_device() {
     HIP_TRY(hipMalloc(&d_gen, (size_t)n * 4));
     HIP_TRY(hipMalloc(&d_effgen, (size_t)n * 4));
     HIP_TRY(hipMalloc(&d_sent, (size_t)n * 8));
+    {
+        const unsigned long long init[4] = {~0ull, 0ull, 0ull, 0ull};
+        HIP_TRY(hipMalloc(&d_phase_ts, sizeof(init)));
+        HIP_TRY(hipMemcpy(d_phase_ts, init, sizeof(init), hipMemcpyHostToDevice));
+    }
     HIP_TRY(hipMemsetAsync(d_recv, 0, (size_t)n * 4, stream));
     HIP_TRY(hipMemsetAsync(d_gen, 0, (size_t)n * 4, stream));
     HIP_TRY(hipMemsetAsync(d_effgen, 0, (size_t)n * 4, stream));
@@ -1994,26 +2010,18 @@ int gossip_engine::tick_step_a(int64_t t) {
         };
         hipEvent_t e0 = nullptr, e1 = nullptr, p0 = nullptr, p1 = nullptr;
         a.inc = nullptr;
-        // DENSE phase = transpose + MFMA + dedup, timed as ONE unit: an event before the transpose
-        // and one after the last dedup on the engine stream (a sum of per-kernel event pairs
-        // misreads 10-us kernels; the span is what the phase costs, launch gaps included)
+        // DENSE phase = transpose + MFMA + dedup, timed as ONE unit (below)
         const bool dense_timing = dense && (cfg.flags & GOSSIP_F_TIMING);
-        auto phase_begin = [&]() -> hipEvent_t {
-            if (!dense_timing) return nullptr;
-            hipEvent_t x = get_event();
-            return hipEventRecord(x, stream) == hipSuccess ? x : nullptr;
-        };
-        auto phase_end = [&](hipEvent_t x) {
-            if (!x) return;
-            hipEvent_t y = get_event();
-            if (hipEventRecord(y, stream) == hipSuccess) timers_phase.emplace_back(x, y);
-        };
-        hipEvent_t dense_ph0 = nullptr;  // the DENSE phase's start (phase_end after the dedup)
+        // The DENSE phase is timed on the device: the first k_transpose block's start and the last
+        // k_dense_dedup block's end (s_memrealtime, 100 MHz), accumulated per tick by
+        // k_phase_acc -- the span a kernel trace shows.  An event pair around the phase also
+        // counted the host's launch latency: 273 us against a 136 us span on C2 (profiles/r04).
+        unsigned long long* pts = dense_timing ? d_phase_ts : nullptr;
+        a.phase_ts = pts;
         if (dense) {  // transpose the frontier to share-column bit rows (not timed as the pull)
-            dense_ph0 = phase_begin();
             dim3 eg(n_pad / 256u, wact);
             k_transpose<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad / 32u, wact, a.live_prev,
-                                                d_nz[fcur], ntw, d_FT);
+                                                d_nz[fcur], ntw, d_FT, pts);
             HIP_TRY(hipGetLastError());
         }
         // young tiles beside k_pull: the two kernels touch disjoint words; they share the per-node
@@ -2145,7 +2153,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 if (rc) return rc;
                 if ((rc = end_chunk(c))) return rc;
             }
-            phase_end(dense_ph0);  // (row chunks: the chunks' births are inside the span)
+            if (pts) k_phase_acc<<<1, 1, 0, stream>>>(pts);  // (row chunks: the chunks' births are inside the span)
         } else if (dense) {
             // The timed kernel in DENSE mode is the MFMA contraction (pull_ms); its incoming
             // words are then consumed by k_dense_dedup.  The whole phase -- transpose, MFMA,
@@ -2158,7 +2166,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             }
             a.inc = d_inc;
             run_dedup(a);
-            phase_end(dense_ph0);
+            if (pts) k_phase_acc<<<1, 1, 0, stream>>>(pts);
         } else if (opt_rehearse_rows > 1 && !ny) {
             // row-partition rehearsal: one pull launch per rank's row range, each timed
             for (uint32_t r = 0; r + 1 < (uint32_t)rr_lo.size(); r++) {
@@ -3665,6 +3673,11 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
         e->young_ms_done = yms;
         c->young_ms = yms;
         double pms = e->phase_ms_done;
+        if (e->dense && e->d_phase_ts) {  // device-stamped DENSE spans (100 MHz ticks)
+            unsigned long long ts[4];
+            HIP_TRY(hipMemcpy(ts, e->d_phase_ts, sizeof(ts), hipMemcpyDeviceToHost));
+            pms += (double)ts[2] * 1e-5;
+        }
         for (auto& p : e->timers_phase) {
             float x = 0.f;
             HIP_TRY(hipEventElapsedTime(&x, p.first, p.second));
@@ -3760,6 +3773,7 @@ int gossip_engine_reset_timing(gossip_engine* e) {
     }
     e->timers_phase.clear();
     e->phase_ms_done = 0.0;
+    if (e->d_phase_ts) HIP_TRY(hipMemsetAsync(e->d_phase_ts + 2, 0, 16, e->stream));
     e->rehearse_harvest();  // (row-partition rehearsal: restart the per-range sums)
     for (auto& v : e->rr_ms) std::fill(v.begin(), v.end(), 0.0);
     std::fill(e->rr_bytes.begin(), e->rr_bytes.end(), 0ull);
