@@ -939,20 +939,21 @@ int gossip_engine::prepare_instances() {
     const bool any_collision = gossip::any_id_collision(m, ev.data());
     if (any_collision) compute_components();
     // Key each event by (id, component); singles use their own index.
+    // (the phase and time ride in the key: the sort touches no event)
     struct Key {
         uint32_t id, comp, ev;
+        int64_t ph, ns;
     };
     std::vector<Key> keys(m);
     for (uint64_t k = 0; k < m; k++) {
         const gossip_gen_event& e = ev[k];
-        keys[k] = Key{e.share_id, any_collision ? comp[e.node] : 0u, (uint32_t)k};
+        keys[k] = Key{e.share_id, any_collision ? comp[e.node] : 0u, (uint32_t)k, e.ns % L, e.ns};
     }
-    std::sort(keys.begin(), keys.end(), [&](const Key& a, const Key& b) {
+    std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) {
         if (a.id != b.id) return a.id < b.id;
         if (a.comp != b.comp) return a.comp < b.comp;
-        const int64_t pa = ev[a.ev].ns % L, pb = ev[b.ev].ns % L;  // phase order
-        if (pa != pb) return pa < pb;
-        return ev[a.ev].ns != ev[b.ev].ns ? ev[a.ev].ns < ev[b.ev].ns : a.ev < b.ev;
+        if (a.ph != b.ph) return a.ph < b.ph;  // phase order
+        return a.ns != b.ns ? a.ns < b.ns : a.ev < b.ev;
     });
     // Shard ownership: deterministic hash of the instance key.
     const uint32_t S = cfg.shard_count > 1 ? cfg.shard_count : 1;
@@ -2991,7 +2992,13 @@ int gossip_engine_set_graph(gossip_engine* e, uint32_t num_nodes, const int64_t*
 int gossip_engine_set_topology(gossip_engine* e, const gossip_topology* t) {
     if (!t) return set_error(GOSSIP_EINVAL, "NULL topology");
     int rc = gossip_engine_set_graph(e, t->n, t->row_ptr.data(), t->col.data(), t->mult.data());
-    if (rc || !e->handshake) return rc;
+    if (rc) return rc;
+    try {
+        gossip::cached_topology_components(t, &e->comp);  // same graph: reuse the labels if built
+    } catch (const std::bad_alloc&) {
+        return set_error(GOSSIP_ENOMEM, "host allocation failed");
+    }
+    if (!e->handshake) return rc;
     // Handshake window: key (a,b) puts b in peers(a) at makeconnections (p2pnetwork.cc:144-145)
     // and a in peers(b) only when REGISTER arrives (p2pnode.cc:185-186).  Until then v sends
     // to its |keys (v,*)| connector-side peers, and the shares that get through (sent in

@@ -11,6 +11,7 @@
 //   PrintStatistics           p2pnetwork.cc:253-285
 //   PrintPeriodicStats        p2pnetwork.cc:231-250
 #include <algorithm>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -182,6 +183,21 @@ std::vector<uint32_t> components(uint32_t n, const int64_t* row_ptr, const int32
     return comp;
 }
 
+static std::mutex g_comp_mu;
+
+const std::vector<uint32_t>& topology_components(const gossip_topology* t) {
+    std::lock_guard<std::mutex> g(g_comp_mu);
+    if (t->comp.empty() && t->n) t->comp = components(t->n, t->row_ptr.data(), t->col.data());
+    return t->comp;
+}
+
+bool cached_topology_components(const gossip_topology* t, std::vector<uint32_t>* out) {
+    std::lock_guard<std::mutex> g(g_comp_mu);
+    if (t->comp.empty()) return false;
+    *out = t->comp;
+    return true;
+}
+
 uint64_t instance_hash(uint32_t share_id, uint32_t node_or_comp, bool lone) {
     uint64_t x = ((uint64_t)share_id << 32) ^ node_or_comp ^ (lone ? 0x9e3779b97f4a7c15ull : 0ull);
     x ^= x >> 33;
@@ -209,19 +225,27 @@ extern "C" int gossip_shard_events(const gossip_topology* t, uint64_t m, const g
                                    uint32_t shard_count, uint32_t* owner) {
     if (!t || (m && (!ev || !owner))) return set_error(GOSSIP_EINVAL, "NULL argument");
     if (shard_count == 0) return set_error(GOSSIP_EINVAL, "shard_count must be >= 1");
+    if (m >= (1ull << 32)) return set_error(GOSSIP_EINVAL, "more than 2^32 - 1 events");
     try {
-        std::vector<uint32_t> ids(m);
-        for (uint64_t k = 0; k < m; k++) ids[k] = ev[k].share_id;
-        std::sort(ids.begin(), ids.end());
-        std::vector<uint32_t> comp;
-        if (any_id_collision(m, ev)) comp = components(t->n, t->row_ptr.data(), t->col.data());
-        for (uint64_t k = 0; k < m; k++) {
+        for (uint64_t k = 0; k < m; k++)
             if (ev[k].node >= t->n) return set_error(GOSSIP_EINVAL, "event node out of range");
-            const uint32_t id = ev[k].share_id;
-            const auto range = std::equal_range(ids.begin(), ids.end(), id);
-            const bool lone = (range.second - range.first) == 1;
-            const uint64_t h = lone ? instance_hash(id, ev[k].node, true)
-                                    : instance_hash(id, comp[ev[k].node], false);
+        // one sort of (id, event index): runs of equal ids give both the collision test and
+        // every event's lone flag
+        std::vector<uint64_t> key(m);
+        for (uint64_t k = 0; k < m; k++) key[k] = ((uint64_t)ev[k].share_id << 32) | k;
+        std::sort(key.begin(), key.end());
+        std::vector<uint8_t> lone(m, 1);
+        bool collision = false;
+        for (uint64_t k = 1; k < m; k++)
+            if ((key[k] >> 32) == (key[k - 1] >> 32)) {
+                lone[(uint32_t)key[k]] = lone[(uint32_t)key[k - 1]] = 0;
+                collision = true;
+            }
+        key = std::vector<uint64_t>();
+        if (collision) topology_components(t);
+        for (uint64_t k = 0; k < m; k++) {
+            const uint64_t h = lone[k] ? instance_hash(ev[k].share_id, ev[k].node, true)
+                                       : instance_hash(ev[k].share_id, t->comp[ev[k].node], false);
             owner[k] = (uint32_t)(h % shard_count);
         }
         return GOSSIP_OK;

@@ -31,6 +31,8 @@ struct gossip_topology {
     std::vector<uint8_t> mult;     // multiplicity of col in peers(row): 1 or 2
     std::vector<uint32_t> peers;   // |peers(v)| including duplicates
     std::vector<uint32_t> sockets; // |peersockets(v)| = distinct peers
+    // connected-component labels, built on first use by gossip_shard_events (guarded there)
+    mutable std::vector<uint32_t> comp;
 };
 
 struct gossip_schedule {
@@ -48,6 +50,10 @@ std::vector<uint32_t> components(uint32_t n, const int64_t* row_ptr, const int32
 // shareId inside one connected component; a lone generation of an id is keyed by
 // (id, node) so that no component labelling is needed when no id collides.
 uint64_t instance_hash(uint32_t share_id, uint32_t node_or_comp, bool lone);
+// The topology's component labels, built once and cached on it (thread-safe).
+const std::vector<uint32_t>& topology_components(const gossip_topology* t);
+// Copies the cached labels into *out when an earlier call built them.
+bool cached_topology_components(const gossip_topology* t, std::vector<uint32_t>* out);
 
 // True if any two events share an id.
 bool any_id_collision(uint64_t m, const gossip_gen_event* ev);

@@ -148,16 +148,15 @@ def test_c4_sample_matches_oracle_a(gossip, oracle, c4):
     # variants below
     pool = ThreadPoolExecutor(1)
     fut = pool.submit(oracle.run_replay, n, W.L_NS, W.T0_NS, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"])
-    # (the sample's window is <= 16 words: the pull is k_pull<8..16, 1>, whatever pull_lpw says)
+    # (the sample's window is <= 16 words: the pull is k_pull<8..16, 1>, whatever pull_lpw says;
+    # young_overlap 0 and pull_gate 0 are test_young_gpu's and test_late_exit_gpu's)
     variants = [
         ("auto (this 11-generation sample is too thin for young tiles)", ()),
         ("young-tile slots forced on", (("young", 1),)),
         ("young tiles, 8-entry slots (overflow paths at scale)", (("young", 1), ("young_cap", 8))),
-        ("young tiles after k_pull on one stream", (("young", 1), ("young_overlap", 0))),
         ("nt rows, 16384-block grid (k_pull<8..16,1,false>: this sample's window is <= 16 words; "
          "the production k_pull<32,1,true> is test_c4_headline_kernels_match_oracle_b's)", (("pull_nt", 1), ("pull_grid", 16384))),
         ("nt rows, 3-block grid", (("pull_nt", 1), ("pull_grid", 3))),
-        ("every live seen pair read (no occupancy gate)", (("pull_gate", 0),)),
         ("no bottom-up early exit (late_age 0; the default exits on every tile)", (("late_age", 0),)),
     ]
     runs = []
