@@ -232,9 +232,11 @@ def test_c4_headline_kernels_match_oracle_b(gossip, oracle, c4):
             assert c.pull_sat == 1 and c.pull_sat_skips > 0, name
 
 
-def _c4_shard_deltas(gossip, topo, ev, shard, shards, t0, t1):
+def _c4_shard_deltas(gossip, topo, ev, shard, shards, t0, t1, options=()):
     W = _w()
     eng = gossip.Engine(topo.num_nodes, W.L_NS, W.T0_NS, W.T_CUT_NS, shard_rank=shard, shard_count=shards)
+    for k, v in options:
+        eng.set_option(k, v)
     eng.set_topology(topo)
     eng.set_schedule(ev)
     eng.run(t0)
@@ -253,8 +255,9 @@ def test_c4_bench_slice_equals_continuous_run(gossip, c4):
     # timed over ticks [2005, 2025).  Pinned here against the CONTINUOUS run (every generation
     # from t = 5 s) of the same share shard: the per-node recv deltas and the edge events of the
     # timed ticks must be identical (p2pnode.cc:189: an id's earlier floods are in the seen-sets
-    # either way).  Shard 0 of 4: the continuous run's start-up (the renewal density peaks ~7 s)
-    # needs ~25 % more live words than the steady state, more than half the shares fit one card.
+    # either way).  Shard 0 of 8 (the 8-GPU layout's share shard): the continuous run's start-up
+    # (the renewal density peaks ~7 s) needs ~25 % more live words than the steady state, and
+    # the eighth keeps the 1,000 ticks from t = 5 s short.
     W = _w()
     topo = c4[0]
     n = topo.num_nodes
@@ -265,15 +268,18 @@ def test_c4_bench_slice_equals_continuous_run(gossip, c4):
     assert info["earlier_same_id"] > 0
     ev_c = gossip.make_schedule(n, W.CONFIGS["C4"]["node_seed"], W.T0_NS, W.T_CUT_NS, t_gen_end_ns=t1 * W.L_NS,
                                 threads=16)
-    shards = 4
+    shards = 8
     own_s, own_c = gossip.shard_events(topo, ev_s, shards), gossip.shard_events(topo, ev_c, shards)
     # the slice's events are a subset of the continuous run's, each on the same shard
     key = lambda e: (e["ns"].astype(np.int64) << 24) | e["node"].astype(np.int64)  # noqa: E731 (ns < 2^34, n < 2^24)
     sl_in_c = np.isin(key(ev_c), key(ev_s))
     assert int(sl_in_c.sum()) == len(ev_s)
     assert np.array_equal(own_c[sl_in_c], own_s)
-    a0, a1, ca0, ca1 = _c4_shard_deltas(gossip, topo, ev_s, 0, shards, t0, t1)
-    b0, b1, cb0, cb1 = _c4_shard_deltas(gossip, topo, ev_c, 0, shards, t0, t1)
+    # young tiles forced on: auto turns them off at 8 shards (~12 slot entries per node, §3), the
+    # 2-shard bench runs them
+    yo = (("young", 1),)
+    a0, a1, ca0, ca1 = _c4_shard_deltas(gossip, topo, ev_s, 0, shards, t0, t1, yo)
+    b0, b1, cb0, cb1 = _c4_shard_deltas(gossip, topo, ev_c, 0, shards, t0, t1, yo)
     for k in ("recv", "gen", "sent", "processed"):
         da = getattr(a1, k).astype(np.int64) - getattr(a0, k).astype(np.int64)
         db = getattr(b1, k).astype(np.int64) - getattr(b0, k).astype(np.int64)
@@ -288,7 +294,7 @@ def test_c4_bench_slice_equals_continuous_run(gossip, c4):
     # later generations of ids whose earlier flood already covered the node: counted, not processed
     assert int((a1.gen.astype(np.int64) + a1.recv - a1.processed).sum()) > 0
     assert ca1.words_hw > 200 and int(a1.recv.sum()) > 100 * len(gens)
-    # the production pull: young-tile slots chosen automatically, the early exit on every tile
+    # the bench's pull: young-tile slots, the early exit on every tile
     assert ca1.young_launches > 0 and ca1.pull_late_age == 1
 
 
