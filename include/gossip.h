@@ -286,7 +286,7 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *                      (zeros included) and read the next tick without occupancy words: -1 auto
  *                      (BFS layer model of the graph, default), 0 off, 1 every listed tile
  *                      (tests)                                                [GOSSIP_DENSE_ROWS]
- *   "young_grid"       k_pull_young blocks, 0 = the pull grid                [GOSSIP_YOUNG_GRID]
+ *   "young_grid"       k_pull_young blocks, 0 = twice the pull grid          [GOSSIP_YOUNG_GRID]
  *   "young_list_cap"   seen-list entries per node (1..127, default 127): beyond it a list overflows
  *                      to dense seen rows (tests: small lists exercise the overflow paths)
  *   "young_nt"         1: k_pull_young reads its peers' slot lines non-temporally (default), 0:
