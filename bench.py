@@ -43,8 +43,19 @@ import gossip.workloads as WL  # noqa: E402
 # BASELINE.json "metric", quoted on C4 (10M nodes)
 BASELINE_METRIC = "share-deliveries/sec (edge events) at 10M nodes, 1/2/4/8 GPUs; % HBM/MFMA peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# the engine's young_overlap option (include/gossip.h), default 1; GOSSIP_YOUNG_OVERLAP sets it
-YOUNG_OVERLAP = int(os.environ.get("GOSSIP_YOUNG_OVERLAP", "1"))
+# Every engine option that shapes the pull launches (include/gossip.h), read back from the engine
+# and recorded in the line's pull_variant: committed PMC traffic attaches only to a line whose
+# variant -- these values, the resolved young grid and the library build -- equals the pass's
+LAUNCH_OPTIONS = ("pull_nt", "pull_grid", "pull_gate", "pull_tiles", "pull_tile_order",
+                  "pull_sat", "dense_rows", "late_age", "young", "young_age", "young_cap",
+                  "young_list_cap", "young_nt", "young_overlap", "young_grid")
+
+
+def lib_build_id():
+    """sha256 (first 16 hex digits) of the libgossip.so this process loaded."""
+    import hashlib
+    with open(gossip.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 T0_NS = 5_000_000_000
 SLICE_NS = 10_000_000_000  # steady-state slice start (tick 2000 at 5 ms)
 L_NS = 5_000_000
@@ -131,6 +142,28 @@ def cpu_baseline_bitsliced(topo, ev, sample_shares, hops, threads):
                        f"propagation (host nproc {os.cpu_count()})")
 
 
+def young_breakdown(acc, launches, n):
+    """k_pull_young's algorithmic bytes per launch, item by item: the terms of the engine's
+    young_bytes_moved (engine.hip, gossip_engine_get_counters), so the items add up to
+    bytes_per_launch (tests/test_bench_pmc.py)."""
+    yl = max(launches, 1)
+    return {
+        "slot_lines_read": 128 * acc["young_sl"] / yl,
+        "fallback_rows_read": 128 * acc["young_fb"] / yl,
+        "peer_ids_and_hints": 5 * acc["young_col_ids"] / yl,
+        "own_seen_read": 8 * acc["young_seen_reads"] / yl,
+        "own_seen_write": 8 * acc["young_seen_writes"] / yl,
+        "dense_rows_written": 128 * acc["young_rows_written"] / yl,
+        "slot_lines_written": 128 * acc["young_slot_writes"] / yl,
+        "unhinted_second_lines_read": 128 * acc.get("young_line2_misses", 0) / yl,
+        # seen rows written whole: the lists of tiles leaving the young set materialised, and
+        # fresh tiles cleared at nodes whose list overflowed (young_fresh_lines)
+        "seen_rows_written_whole": 128 * acc.get("young_fresh_lines", 0) / yl,
+        "seen_list_lines_read_written": 128 * acc.get("young_list_lines", 0) / yl,
+        "per_node_rowptr_counters": 8.0 * (n + 1) + 16.0 * n,
+    }
+
+
 def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, flags):
     """Warm up and time every shard this rank owns; raises gossip.GossipError on failure."""
     W, K = args.warmup, args.steps
@@ -143,6 +176,7 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
         t_eng = time.perf_counter()
         eng = gossip.Engine(wl["nodes"], L_NS, T0_NS, T_CUT_NS, device=local, flags=flags,
                             shard_rank=s, shard_count=shards)
+        acc["options"] = {k: eng.get_option(k) for k in LAUNCH_OPTIONS}
         try:
             eng.set_topology(topo)
             eng.set_schedule(ev)
@@ -179,7 +213,7 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
         acc["young_sl"] += c1.young_slot_lines
         acc["young_fb"] += c1.young_fallback_rows
         for k in ("young_col_ids", "young_seen_reads", "young_seen_writes", "young_rows_written",
-                  "young_slot_writes", "young_line2_misses", "young_fresh_lines"):
+                  "young_slot_writes", "young_line2_misses", "young_fresh_lines", "young_list_lines"):
             acc[k] = acc.get(k, 0) + getattr(c1, k)
         acc["phase_ms"] += c1.pull_phase_ms
         acc["words_hw"] = max(acc["words_hw"], c1.words_hw)
@@ -189,6 +223,7 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
         acc["late_age"] = c1.pull_late_age
         acc["pull_tiles"] = c1.pull_tiles
         acc["lpw"], acc["pull_sat"] = c1.pull_lpw, c1.pull_sat
+        acc["young_grid"] = c1.young_grid
         acc["dense_tiles"] = max(acc.get("dense_tiles", 0), c1.pull_dense_tiles)
         # (device-side tallies restart at reset_timing: c1 holds the timed ticks alone)
         acc["sat_skips"] = acc.get("sat_skips", 0) + c1.pull_sat_skips
@@ -253,8 +288,10 @@ def rehearse_rows(args, wl, topo, ev, shards, R, flags):
         "rank_ingress_bytes_per_tick": ingress.tolist(),
         "rank_ingress_bytes_per_tick_max": float(ingress.max()),
         "unpartitioned_pull_ms_per_tick": c1.pull_ms / max(c1.pull_launches, 1),
-        # + the exchange buffers a rank would hold: its own message and the R - 1 it receives
-        "rank_device_gib": (fbytes + c1.words_cap * 8 * int(own_rows.max()) + R * float(msg.max())) / 2**30,
+        # + the exchange buffers a rank would hold: its own message and the R - 1 it receives, each
+        # sized for the largest message of a tick (not the mean: ADVICE r04)
+        "message_bytes_per_tick_max": rh["msg_bytes_max"].astype(np.float64).tolist(),
+        "rank_device_gib": (fbytes + c1.words_cap * 8 * int(own_rows.max()) + R * float(rh["msg_bytes_max"].max())) / 2**30,
         "wall_s_rehearsal": wall,
         "window_words": c1.words_hw,
     }
@@ -276,6 +313,10 @@ def main():
     ap.add_argument("--rehearse-shards", type=int, default=0,
                     help="diagnostic: run only shard 0 of S on this one GPU (per-rank footprint "
                          "and time of an S-GPU run); the JSON line is marked REHEARSAL")
+    ap.add_argument("--shard-rule", choices=["hash", "tick"], default="hash",
+                    help="share-shard rule: hash of the instance key (default) or the birth tick of "
+                         "its first generation (GOSSIP_F_SHARD_BY_TICK: a shard's births of a tick "
+                         "fill whole tiles of one age)")
     ap.add_argument("--rehearse-rows", type=int, default=0,
                     help="diagnostic: one rank of an R-rank row partition of share shard 0 of "
                          "--rehearse-shards (default: the workload's fit) on this one GPU")
@@ -320,7 +361,8 @@ def main():
     t_gen_end = SLICE_NS + (W + K + 1) * L_NS
     ev, sinfo = WL.slice_schedule(n, WL.CONFIGS[args.workload]["node_seed"], SLICE_NS, t_gen_end,
                                   threads=args.threads)
-    flags = gossip.F_TIMING | (gossip.F_NOSKIP if args.noskip else 0)
+    flags = gossip.F_TIMING | (gossip.F_NOSKIP if args.noskip else 0) | \
+        (gossip.F_SHARD_BY_TICK if args.shard_rule == "tick" else 0)
     if rank == 0:
         rp, _, _ = topo.csr()
         log(f"[bench] {wl['desc']}: {topo.num_nodes} nodes, {int(rp[-1])} directed entries, "
@@ -417,6 +459,7 @@ def main():
                 "window_early_retires": acc.get("early_retires", 0),
                 "device_gib": acc["dev_bytes"] / 2**30,
                 "parallelism": f"share-shard x{shards} over {max(world, 1)} rank(s)",
+                "shard_rule": args.shard_rule,
             },
             "roofline": None,
         }
@@ -446,22 +489,28 @@ def main():
                     acc["moved"] - 16 * acc["pe"] - 4 * acc["col"] - 8 * acc["nz"] -
                     16 * (acc["srd"] + acc["swr"] + acc["fwr"])),
             },
+            "breakdown_sums_to_bytes": True,  # (the last item is the remainder of the engine's count)
             "saturated_tiles_skipped_per_launch": per_launch(acc.get("sat_skips", 0)),
             "items_per_launch": per_launch(acc.get("items", 0)),
             "gather_items_per_launch": per_launch(acc.get("gather_items", 0)),
             "dense_row_tiles_last_tick": acc.get("dense_tiles", 0),
         }
+        opts = acc.get("options", {})
+        overlap = opts.get("young_overlap", 1)
         variant = {"nt_rows": acc["nt"], "grid": acc["grid"],
-                   "young_overlap": YOUNG_OVERLAP if acc["young_launches"] else None,
+                   "young_overlap": overlap if acc["young_launches"] else None,
                    "late_age": acc.get("late_age", 0), "pull_tiles": acc.get("pull_tiles", 0),
                    "lanes_per_node": acc.get("lpw", 0), "pull_sat": acc.get("pull_sat", 0),
-                   "dense_rows": 1 if acc.get("dense_tiles", 0) else 0}
+                   "dense_rows": 1 if acc.get("dense_tiles", 0) else 0,
+                   "young_grid_blocks": acc.get("young_grid", 0) if acc["young_launches"] else None,
+                   "options": opts, "lib_sha256": lib_build_id()}
         t_pull, why_pull = pmc_traffic(wl["name"], out, variant)
         k_pull["traffic"] = t_pull
         young = None
         if acc["young_launches"]:
             yl = acc["young_launches"]
             y_ms = acc["young_ms"] / yl
+            ybd = young_breakdown(acc, yl, n)
             young = {
                 "kernel": "k_pull_young",
                 "avg_launch_ms": y_ms,
@@ -471,17 +520,8 @@ def main():
                 "slot_lines_per_launch": acc["young_sl"] / yl,
                 "fallback_rows_per_launch": acc["young_fb"] / yl,
                 "second_lines_unhinted_per_launch": acc.get("young_line2_misses", 0) / yl,
-                "bytes_breakdown_per_launch": {
-                    "slot_lines_read": 128 * acc["young_sl"] / yl,
-                    "fallback_rows_read": 128 * acc["young_fb"] / yl,
-                    "peer_ids_and_hints": 5 * acc["young_col_ids"] / yl,
-                    "own_seen_read": 8 * acc["young_seen_reads"] / yl,
-                    "own_seen_write": 8 * acc["young_seen_writes"] / yl,
-                    "dense_rows_written": 128 * acc["young_rows_written"] / yl,
-                    "slot_lines_written": 128 * acc["young_slot_writes"] / yl,
-                    "unhinted_second_lines_read": 128 * acc.get("young_line2_misses", 0) / yl,
-                    "fresh_tile_seen_lines_cleared": 128 * acc.get("young_fresh_lines", 0) / yl,
-                },
+                "bytes_breakdown_per_launch": ybd,
+                "breakdown_sums_to_bytes": abs(sum(ybd.values()) - acc["young_bytes"] / yl) <= 1e-6 * acc["young_bytes"] / yl,
             }
             t_young, why_young = pmc_traffic(wl["name"] + "_young", out, variant)
             young["traffic"] = t_young
@@ -507,7 +547,7 @@ def main():
                 "frac": ph_ach / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "kernel": "pull phase: k_pull + k_pull_young" +
-                          (" (concurrent, two streams)" if YOUNG_OVERLAP else " (in sequence)"),
+                          (" (concurrent, two streams)" if overlap else " (in sequence)"),
                 "avg_launch_ms": ph_ms,
                 "launches": launches,
                 "bytes_per_launch": ph_b,

@@ -128,6 +128,11 @@ void gossip_schedule_destroy(gossip_schedule* s);
  * the shard that simulates event k.  Generations sharing an id inside one connected
  * component (one seen-set entry, p2pnode.cc:189) always land on the same shard, so shards
  * never interact and per-node counters add up exactly across shards. */
+/* The birth-tick rule (GOSSIP_F_SHARD_BY_TICK): owner[k] = (floor(first ns of k's instance /
+ * latency_ns)) mod shard_count, the instance being k's (id, node) when k's id is unique and its
+ * (id, connected component) otherwise -- colliding-id instances stay whole. */
+int gossip_shard_events_by_tick(const gossip_topology* t, uint64_t num_events, const gossip_gen_event* ev,
+                                uint32_t shard_count, int64_t latency_ns, uint32_t* owner);
 int gossip_shard_events(const gossip_topology* t, uint64_t num_events, const gossip_gen_event* ev,
                         uint32_t shard_count, uint32_t* owner);
 
@@ -179,6 +184,12 @@ typedef struct gossip_config {
                                   node's peers are its connector-side keys only.  Needs
                                   gossip_engine_set_topology, CSR mode, t_start % latency == 0
                                   and t_cut >= t_start + 3 latency.                          */
+#define GOSSIP_F_SHARD_BY_TICK 256u /* share shards (shard_count > 1) by birth tick: an instance
+                                       belongs to shard (tick of its first generation) mod
+                                       shard_count instead of a hash of its key, so a shard's
+                                       births of a tick fill whole tiles of one age
+                                       (gossip_shard_events_by_tick; every engine of a job must
+                                       use the same rule)                                        */
 
 int gossip_engine_create(const gossip_config* cfg, gossip_engine** out);
 /* Graph: CSR over distinct neighbours with multiplicity in {1,2} (see topology above). */
@@ -263,14 +274,13 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *   "pull_nt"          -1 auto (non-temporal rows when the live frontier n x wact x 8 B exceeds
  *                      16 GiB), 0 / 1 forced                              [GOSSIP_PULL_NT]
  *   "pull_grid"        blocks per pull launch, 0 = auto (16,384 non-temporal, else 4,096)
- *   "pull_lds_min"     LDS bytes every k_pull block reserves at least (0 = what it uses): caps
- *                      k_pull's blocks per CU so that k_pull_young blocks fit beside them
  *                                                                         [GOSSIP_PULL_GRID]
  *   "pull_tile_order"  1: k_pull's tile lists in age order inside each occupancy word (default),
  *                      0: in tile order                                [GOSSIP_PULL_TILE_ORDER]
- *   "pull_lpw"         word-lanes per node for windows > 64 words: 0 auto (32), 16, 32, 64
- *                                                                         [GOSSIP_PULL_LPW]
  *   "dense_min_tiles"  MFMA block tiles the K split aims for (512)  [GOSSIP_DENSE_MIN_TILES]
+ *   "dense_fused"      1: a DENSE tick runs as one k_dense_fused launch when it can (no id-group
+ *                      words, no row partition, no no-skip diagnostic; the default), 0: always
+ *                      k_transpose + k_dense_bits + k_dense_dedup            [GOSSIP_DENSE_FUSED]
  *   "young"            young-tile slots (k_pull_young): -1 auto (CSR tick engine, n >= 2^20),
  *                      0 off, 1 on (before the schedule)                    [GOSSIP_YOUNG]
  *   "young_age"        tiles stay in slots while their oldest shares are <= this many hops (5)
@@ -292,9 +302,8 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *   "young_nt"         1: k_pull_young reads its peers' slot lines non-temporally (default), 0:
  *                      cached                                                  [GOSSIP_YOUNG_NT]
  *   "young_overlap"    0: k_pull_young after k_pull on the engine stream; 1: the two run
- *                      concurrently on two streams, k_pull_young launched first (default);
- *                      2: concurrently, k_pull launched first; 3 / 4: as 1 with the second
- *                      stream at the lowest / highest priority          [GOSSIP_YOUNG_OVERLAP]
+ *                      concurrently on two streams, k_pull_young launched first (default)
+ *                                                                   [GOSSIP_YOUNG_OVERLAP]
  *   "mem_limit"        bytes of device memory the engine may hold, 0 = what the device has
  *                      free; a window that outgrows it fails with GOSSIP_ECAPACITY / ENOMEM
  *                      (callers then split the shares into more shards)   [GOSSIP_MEM_LIMIT]
@@ -312,6 +321,9 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *                      GOSSIP_F_TIMING -- one rank's compute and exchange work, measured on one
  *                      GPU over the whole graph's data (gossip_engine_get_rehearsal) */
 int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value);
+/* The value an option holds (what set_option or its environment default set; 0 / -1 = auto where
+ * the table above says so).  GOSSIP_EINVAL for an unknown name. */
+int gossip_engine_get_option(const gossip_engine* e, const char* name, int64_t* value);
 /* The mode the engine runs (AUTO resolves at gossip_engine_set_graph). */
 int gossip_engine_mode(const gossip_engine* e);
 /* First tick of the run window (floor(t_start/L)) and one past the last tick. */
@@ -391,12 +403,20 @@ typedef struct gossip_counters {
     uint64_t young_list_lines;   /* seen-list lines k_pull_young read and wrote [128 B] since reset */
     uint64_t pull_items;         /* k_pull work items (node, pass) since reset */
     uint64_t pull_gather_items;  /* of those, items that gathered some peer row since reset */
+    uint64_t dense_fused_launches; /* DENSE ticks run as one k_dense_fused launch (contraction + dedup +
+                                      transposed F_next) since creation; the others ran k_transpose,
+                                      k_dense_bits and k_dense_dedup (option dense_fused)       */
+    uint32_t young_grid;         /* blocks of the last k_pull_young launch (option young_grid resolved) */
+    uint32_t pad1;
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 /* Option rehearse_rows = R: per row block r < R, summed since the last reset_timing -- pull time,
  * pack time, unpack time (ms, HIP events) and message bytes; *ticks = ticks rehearsed. */
 int gossip_engine_get_rehearsal(gossip_engine* e, uint32_t ranges, double* pull_ms, double* pack_ms,
                                 double* unpack_ms, uint64_t* msg_bytes, uint64_t* ticks);
+/* The same rehearsal: per row block, the largest message of one tick (bytes) since reset_timing --
+ * what a rank's exchange buffers must hold, where get_rehearsal's sums give the mean. */
+int gossip_engine_get_rehearsal_peak(gossip_engine* e, uint32_t ranges, uint64_t* msg_bytes_max);
 int gossip_engine_reset_timing(gossip_engine* e);
 
 /* First-contact trace (GOSSIP_F_TRACE): one record per (node, shareId) whose first

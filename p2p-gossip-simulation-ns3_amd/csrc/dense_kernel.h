@@ -63,10 +63,7 @@ __global__ __launch_bounds__(256) void k_transpose(const uint64_t* __restrict__ 
                                                    uint32_t n, uint32_t kw, uint32_t nwords,
                                                    const unsigned long long* live_prev,
                                                    const unsigned long long* __restrict__ nz,
-                                                   uint32_t ntw, uint32_t* __restrict__ FT,
-                                                   unsigned long long* phase_ts) {
-    // the DENSE phase's start: the earliest block's start time (engine.hip, k_phase_acc)
-    if (phase_ts && threadIdx.x == 0) atomicMin(phase_ts, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+                                                   uint32_t ntw, uint32_t* __restrict__ FT) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t chunk = blockIdx.x * 4u + wave_in_block();  // 64-node chunk
     const uint32_t w = blockIdx.y;
@@ -353,8 +350,361 @@ __global__ __launch_bounds__(1024) void k_dense_dedup(PullArgs a) {
         const unsigned long long have = __hip_atomic_load(&a.live[a.wbase + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (x & ~have) atomicOr(&a.live[a.wbase + i], x);
     }
-    if (a.phase_ts) {  // the DENSE phase's end: the latest block's end time (engine.hip, k_phase_acc)
+}
+
+// ------------------------------------------------------------------------------------------
+// k_dense_fused -- the whole DENSE-mode pull of a tick in ONE persistent kernel (round 5): the
+// contraction Inc = A x F, the dedup against seen (p2pnode.cc:155-165, 189), and the transposed
+// frontier of the NEXT tick, so the tick needs neither k_transpose nor k_dense_dedup nor the
+// incoming-word round trip through HBM.  Round 4 ran the three kernels in sequence: on C2 each
+// dependent launch cost ~6 us of dispatch gap and k_dense_bits itself paid a prologue, a 3-barrier
+// zero-stage test per stage and an epilogue per 256 x 256 tile with nothing to overlap them.
+//
+// Work: one block per CU walks its tiles (256 rows x 256 columns) in an XCD-major order (the
+// column tiles of one row block run on one XCD together, the adjacency rows stay in its L2).
+// Per tile only the K stages whose frontier bits are non-zero are computed: the producer of FT
+// (this kernel's epilogue at t-1, plus k_births) sets a per-(column tile, stage) bit, so an empty
+// stage is neither loaded nor multiplied.  Stages arrive by LDS-DMA (global_load_lds_dwordx4,
+// 16 B per lane, no VGPR staging) into two 64-KB buffers; the next (tile, stage) is issued as soon
+// as the current one has landed -- across tile boundaries, so the next tile's first stage loads
+// while this tile's epilogue runs.  The LDS image is lane-linear per 1-KiB DMA piece (8 rows of
+// 128 B); rows are XOR-swizzled on the SOURCE address -- position p of row r holds 16-B chunk
+// p ^ ((r >> 1) & 7) -- so the 16 lanes of a ds_read_b128 (16 consecutive rows, one chunk) hit 16
+// distinct 16-B bank groups.
+//
+// Epilogue per tile (every column tile of the window, dead ones included, so F_next and FT_next
+// are written whole and need no occupancy test): Inc > 0 -> row words (wave ballots) -> LDS;
+// per (row, word pair) new = inc & ~seen & keep, seen |= new, F_next = new, recv += popcount;
+// then each wave transposes two 64 x 64 bit blocks of `new` (6 shuffle-and-mask steps) into the
+// FT_next rows of its 64 columns, whose non-zero lanes give the word's liveness by ballot.
+// Id groups (WF_GROUP), row partitions and the diagnostic no-skip pull take the three-kernel path
+// (engine.hip decides per tick).
+// ------------------------------------------------------------------------------------------
+struct FusedArgs {
+    const uint32_t* Ab;                    // n_pad rows x kw words of adjacency bits
+    const uint32_t* FTc;                   // transposed F_cur: column rows x kw words
+    uint32_t* FTn;                         // transposed F_next (written for every window column)
+    const unsigned long long* snz_c;       // per column tile nstw words: bit s = stage s of FTc non-zero
+    unsigned long long* snz_n;             // the same for FTn (zeroed by the last tick's launch)
+    unsigned long long* snz_z;             // the buffer the next tick writes: zeroed here
+    uint32_t snz_zwords;
+    uint64_t* seen;
+    uint64_t* Fnext;
+    const WordCtl* ctl;
+    const uint8_t* wflags;
+    uint32_t* recv;
+    unsigned long long* live;              // liveness of this tick
+    const unsigned long long* live_prev;   // nullable: every word live
+    unsigned long long* snap;              // nullable
+    unsigned long long* acct;              // nullable
+    unsigned long long* nz_next;
+    uint32_t ntw;
+    uint32_t n, n_pad, kw, stride;
+    uint32_t nst, nstw;                    // K stages, stage-mask words per column tile
+    uint32_t mb, nt, total;                // row blocks, column tiles, mb * nt
+    uint32_t wact;                         // window words: occupancy bits of tiles < wact / 16
+};
+
+constexpr uint32_t kFStageBytes = 2u * kDenseTile * 128u;  // A + B rows of one 1024-k stage
+constexpr uint32_t kFIncOff = 2u * kFStageBytes;           // 256 rows x 4 words of inc / new
+constexpr uint32_t kFMiscOff = kFIncOff + kDenseTile * 4u * 8u;
+constexpr uint32_t kFLdsBytes = kFMiscOff + 64u;
+static_assert(kStageK == 1024u, "k_dense_fused stages 128-B rows");
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
+
+// One LDS-DMA piece: 16 B per lane from gsrc to LDS byte address lds_dst + 16 x lane.  Inline asm,
+// not __builtin_amdgcn_global_load_lds: for the builtin hipcc cannot tell which LDS bytes the DMA
+// writes and waits vmcnt(0) before every later ds_read -- the next stage's DMA, issued to the other
+// buffer, would then be waited for before the current stage is computed.  The kernel orders the
+// DMA itself (vmcnt(0) + barrier before a buffer is read).  M0 is saved and restored around it.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+// stage s of tile (mblk, ct) into buffer `buf`: wave wid DMAs A rows and B rows [32 wid, 32 wid + 32)
+__device__ __forceinline__ void fused_issue(const FusedArgs& a, uint8_t* S, uint32_t buf, uint32_t mblk, uint32_t ct,
+                                            uint32_t s, uint32_t wid, uint32_t lane) {
+    const uint32_t base = (uint32_t)(uintptr_t)(lds_u8_t*)S + buf * kFStageBytes;
+    const uint32_t rs = lane >> 3, p = lane & 7u;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t row = wid * 32u + j * 8u + rs;
+        const uint32_t q = p ^ ((row >> 1) & 7u);
+        const uint32_t* ga = a.Ab + (uint64_t)(mblk * kDenseTile + row) * a.kw + s * 32u + q * 4u;
+        const uint32_t* gb = a.FTc + (uint64_t)(ct * kDenseTile + row) * a.kw + s * 32u + q * 4u;
+        glds16(ga, base + (wid * 32u + j * 8u) * 128u);
+        glds16(gb, base + kDenseTile * 128u + (wid * 32u + j * 8u) * 128u);
+    }
+}
+
+// the non-empty stages of column tile ct from stage `from` on (bit i of the result = stage from + i,
+// up to 64 stages ahead); every stage when there are no masks (FT from k_transpose)
+__device__ __forceinline__ uint64_t fused_stages(const FusedArgs& a, uint32_t ct, uint32_t from) {
+    if (from >= a.nst) return 0ull;
+    uint64_t m;
+    if (!a.snz_c) {
+        m = ~0ull;
+    } else {
+        const uint32_t wi = from >> 6, sh = from & 63u;
+        m = a.snz_c[(uint64_t)ct * a.nstw + wi] >> sh;
+        if (sh && wi + 1u < a.nstw) m |= a.snz_c[(uint64_t)ct * a.nstw + wi + 1u] << (64u - sh);
+    }
+    const uint32_t left = a.nst - from;
+    return left >= 64u ? m : (m & ((1ull << left) - 1ull));
+}
+
+__device__ __forceinline__ bool fused_tile_live(const FusedArgs& a, uint32_t w0) {
+    if (!a.live_prev) return true;
+    return (a.live_prev[w0] | a.live_prev[w0 + 1] | a.live_prev[w0 + 2] | a.live_prev[w0 + 3]) != 0ull;
+}
+
+// 64 x 64 bit transpose across a wave: lane r holds row r (bit c = column c) on entry, column r
+// (bit r' = row r') on exit
+__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x, uint32_t lane) {
+#pragma unroll
+    for (int j = 32; j >= 1; j >>= 1) {
+        const uint64_t lo = j == 32 ? 0x00000000ffffffffull
+                          : j == 16 ? 0x0000ffff0000ffffull
+                          : j == 8 ? 0x00ff00ff00ff00ffull
+                          : j == 4 ? 0x0f0f0f0f0f0f0f0full
+                          : j == 2 ? 0x3333333333333333ull
+                                   : 0x5555555555555555ull;
+        const uint64_t y = __shfl_xor(x, j, 64);
+        x = (lane & (uint32_t)j) ? ((x & ~lo) | ((y >> j) & lo)) : ((x & lo) | ((y & lo) << j));
+    }
+    return x;
+}
+
+__global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[kFLdsBytes];
+    unsigned long long* sInc = reinterpret_cast<unsigned long long*>(S + kFIncOff);
+    unsigned long long* sMisc = reinterpret_cast<unsigned long long*>(S + kFMiscOff);  // [0..3] live, [4] any
+    const uint32_t t = threadIdx.x, lane = t & 63u, wid = wave_in_block();
+    const uint32_t wm = wid >> 2, wn = wid & 3u;
+    // XCD-major walk: block b runs on XCD b % 8 (speed only); XCD x owns tiles [x per, (x+1) per)
+    const uint32_t nx = gridDim.x >= 8u ? 8u : 1u;
+    const uint32_t xcd = blockIdx.x % nx, bpx = gridDim.x / nx, bi = blockIdx.x / nx;
+    const uint32_t per = (a.total + nx - 1u) / nx;
+    const uint32_t tlo = xcd * per, thi = min(a.total, tlo + per);
+    for (uint32_t i = blockIdx.x * 512u + threadIdx.x; i < a.snz_zwords; i += gridDim.x * 512u) a.snz_z[i] = 0ull;
+    if (bi >= bpx) return;  // (gridDim.x is a multiple of 8 when >= 8)
+
+    const uint32_t h = lane >> 5, rr = lane & 31u, sw = (rr >> 1) & 7u;
+    uint32_t msk[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) msk[e] = 0x01010101u << (4u * h + (uint32_t)e);
+
+    // the (tile, stage) sequence of this block: tiles tlo + bi, + bpx, ... ; stages by mask
+    auto tile_mb = [&](uint32_t T) { return T / a.nt; };
+    auto tile_ct = [&](uint32_t T) { return T % a.nt; };
+    // first stage >= from of tile T (a.nst if none; dead tiles have none)
+    auto first_stage = [&](uint32_t T, uint32_t from) -> uint32_t {
+        const uint32_t ct = tile_ct(T);
+        if (!fused_tile_live(a, ct * 4u)) return a.nst;
+        while (from < a.nst) {
+            const uint64_t m = fused_stages(a, ct, from);
+            if (m) return from + (uint32_t)__builtin_ctzll(m);
+            from += 64u;
+        }
+        return a.nst;
+    };
+    // the next (tile, stage) to load after (T, s): T == thi when none
+    uint32_t LT = tlo + bi, LS = a.nst;
+    while (LT < thi && (LS = first_stage(LT, 0u)) >= a.nst) LT += bpx;
+    uint32_t buf = 0;
+    if (LT < thi) fused_issue(a, S, 0u, tile_mb(LT), tile_ct(LT), LS, wid, lane);
+
+    unsigned long long macs = 0, skipped = 0;
+    uint32_t t_srd = 0, t_swr = 0, t_fwr = 0;
+    unsigned long long snap_local = 0;
+
+    for (uint32_t T = tlo + bi; T < thi; T += bpx) {
+        const uint32_t mblk = tile_mb(T), ct = tile_ct(T), w0 = ct * 4u;
+        v16i_t acc[4][2];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) acc[i][j] = v16i_t{0};
+        uint32_t computed = 0;
+        // the own seen pair of this thread's row (prefetched with the tile's last stage)
+        const uint32_t er = t >> 1, ep = t & 1u;
+        const uint64_t ev = (uint64_t)mblk * kDenseTile + er;
+        const uint32_t wa = w0 + 2u * ep;
+        const uint32_t fa = a.wflags[wa], fb = a.wflags[wa + 1];
+        const uint64_t lpa = a.live_prev ? a.live_prev[wa] : ~0ull, lpb = a.live_prev ? a.live_prev[wa + 1] : ~0ull;
+        const bool dead = (lpa | lpb) == 0ull;
+        const bool need_seen = ev < a.n && (!dead || ((fa | fb) & WF_CLEAR));
+        ulonglong2 s2 = make_ulonglong2(0ull, 0ull);
+        bool seen_loaded = false;
+        while (LT == T) {  // the tile's stages, each already issued into `buf`
+            const uint32_t s = LS;
+            // the next load: this tile's next stage, else the next tile with a stage
+            uint32_t nT = T, nS = s + 1u < a.nst ? first_stage(T, s + 1u) : a.nst;
+            if (nS >= a.nst) {
+                nT = T + bpx;
+                while (nT < thi && (nS = first_stage(nT, 0u)) >= a.nst) nT += bpx;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // stage s landed for every wave; buffer buf ^ 1 is free
+            if (nT < thi) fused_issue(a, S, buf ^ 1u, tile_mb(nT), tile_ct(nT), nS, wid, lane);
+            if (nT != T && need_seen) {  // last stage of the tile: the epilogue's seen pair
+                s2 = *reinterpret_cast<const ulonglong2*>(a.seen + ev * a.stride + wa);
+                seen_loaded = true;
+            }
+            const uint8_t* As = S + buf * kFStageBytes;
+            const uint8_t* Bs = As + kDenseTile * 128u;
+#pragma unroll
+            for (uint32_t kq = 0; kq < kStageQ; kq++) {
+                const uint32_t off = ((kq ^ sw) << 4);
+                uint4 xa[4], xb[2];
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    xa[i] = *reinterpret_cast<const uint4*>(As + (wm * 128u + i * 32u + rr) * 128u + off);
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+                    xb[j] = *reinterpret_cast<const uint4*>(Bs + (wn * 64u + j * 32u + rr) * 128u + off);
+#pragma unroll
+                for (int kc = 0; kc < 4; kc++) {
+                    v4i_t af[4], bf[2];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const uint32_t x = kc == 0 ? xa[i].x : kc == 1 ? xa[i].y : kc == 2 ? xa[i].z : xa[i].w;
+                        af[i] = dense_expand(x, msk);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        const uint32_t x = kc == 0 ? xb[j].x : kc == 1 ? xb[j].y : kc == 2 ? xb[j].z : xb[j].w;
+                        bf[j] = dense_expand(x, msk);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+#pragma unroll
+                        for (int j = 0; j < 2; j++)
+                            acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i][j], 0, 0, 0);
+                }
+            }
+            computed++;
+            buf ^= 1u;
+            LT = nT;
+            LS = nS;
+        }
+        if (need_seen && !seen_loaded) s2 = *reinterpret_cast<const ulonglong2*>(a.seen + ev * a.stride + wa);
+        macs += (unsigned long long)computed;
+        skipped += computed == 0u;
+        // ---- epilogue 1: Inc > 0 -> one 64-bit word per (row, word): wave ballots -> LDS ----
+        if (t < 5u) sMisc[t] = 0ull;
+        {
+            uint64_t lo = 0ull, hi = 0ull;
+            if (computed) {
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int g = 0; g < 16; g++) {
+                        const unsigned long long q0 = __ballot(acc[i][0][g] > 0);
+                        const unsigned long long q1 = __ballot(acc[i][1][g] > 0);
+                        const uint64_t h0 = (q0 & 0xffffffffull) | (q1 << 32);
+                        const uint64_t h1 = (q0 >> 32) | (q1 & 0xffffffff00000000ull);
+                        const uint32_t row = (uint32_t)(i & 1) * 32u + (g & 3) + 8u * (g >> 2);
+                        if (i < 2) {
+                            if (lane == row) lo = h0;
+                            if (lane == row + 4u) lo = h1;
+                        } else {
+                            if (lane == row) hi = h0;
+                            if (lane == row + 4u) hi = h1;
+                        }
+                    }
+            }
+            sInc[(wm * 128u + lane) * 4u + wn] = lo;
+            sInc[(wm * 128u + 64u + lane) * 4u + wn] = hi;
+        }
         __syncthreads();
-        if (threadIdx.x == 0) atomicMax(a.phase_ts + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        // ---- epilogue 2: dedup of (row er, words wa, wa + 1) ----
+        {
+            uint64_t n0 = 0ull, n1 = 0ull;
+            if (ev < a.n) {
+                const uint64_t x0 = sInc[er * 4u + 2u * ep], x1 = sInc[er * 4u + 2u * ep + 1u];
+                if (fa & WF_CLEAR) s2.x = 0ull;
+                if (fb & WF_CLEAR) s2.y = 0ull;
+                const uint64_t k0 = (fa & WF_KEEP) ? a.ctl[wa].keep : ~0ull;
+                const uint64_t k1 = (fb & WF_KEEP) ? a.ctl[wa + 1].keep : ~0ull;
+                n0 = x0 & ~s2.x & k0;
+                n1 = x1 & ~s2.y & k1;
+                const bool swr = (n0 | n1) != 0ull || ((fa | fb) & WF_CLEAR) != 0u;
+                if (swr) *reinterpret_cast<ulonglong2*>(a.seen + ev * a.stride + wa) = make_ulonglong2(s2.x | n0, s2.y | n1);
+                *reinterpret_cast<ulonglong2*>(a.Fnext + ev * a.stride + wa) = make_ulonglong2(n0, n1);
+                t_srd += need_seen;
+                t_swr += swr;
+                t_fwr += 1u;
+                if (a.snap) {
+                    if (fa & WF_SNAP) snap_local += (unsigned long long)__popcll(n0 & a.ctl[wa].snap);
+                    if (fb & WF_SNAP) snap_local += (unsigned long long)__popcll(n1 & a.ctl[wa + 1].snap);
+                }
+                // tile occupancy of F_next: every tile row of the window is written (zeros included)
+                if (ct == 0u && ep == 0u) {
+                    const uint32_t ntl = a.wact / 16u;
+                    for (uint32_t j = 0; j < a.ntw; j++) {
+                        const uint32_t lo_t = j * 64u;
+                        const unsigned long long m = ntl <= lo_t ? 0ull : ntl - lo_t >= 64u ? ~0ull : ((1ull << (ntl - lo_t)) - 1ull);
+                        a.nz_next[ev * a.ntw + j] = m;
+                    }
+                }
+            }
+            uint32_t cnt = (uint32_t)(__popcll(n0) + __popcll(n1));
+            cnt += (uint32_t)__shfl_xor((int)cnt, 1, 64);
+            if (ep == 0u && cnt) atomicAdd(&a.recv[ev], cnt);  // (sent: derived, engine.hip)
+            sInc[er * 4u + 2u * ep] = n0;
+            sInc[er * 4u + 2u * ep + 1u] = n1;
+        }
+        __syncthreads();
+        // ---- epilogue 3: FT_next = new transposed; liveness; the next tick's stage bit ----
+        {
+            unsigned long long any = 0ull;
+#pragma unroll
+            for (uint32_t q = 0; q < 2; q++) {
+                const uint32_t j = wid * 2u + q;         // 64 x 64 block j of the tile's 16
+                const uint32_t wi = j & 3u, rg = j >> 2;  // word, 64-row group
+                const uint64_t x = sInc[(rg * 64u + lane) * 4u + wi];
+                const uint64_t col = wave_transpose64(x, lane);
+                const uint64_t c = (uint64_t)(w0 + wi) * 64u + lane;
+                *reinterpret_cast<uint64_t*>(a.FTn + c * a.kw + mblk * 8u + rg * 2u) = col;
+                const unsigned long long lv = __ballot(col != 0ull);
+                if (lane == 0 && lv) {
+                    atomicOr(&sMisc[wi], lv);
+                    any = 1ull;
+                }
+            }
+            if (lane == 0 && any) atomicOr(&sMisc[4], 1ull);
+        }
+        __syncthreads();
+        if (t < 4u) {
+            const unsigned long long x = sMisc[t];
+            if (x) {
+                const unsigned long long have = __hip_atomic_load(&a.live[w0 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (x & ~have) atomicOr(&a.live[w0 + t], x);
+            }
+        } else if (t == 4u && sMisc[4]) {
+            const uint32_t st = mblk >> 2;  // 4 row blocks of 256 per 1024-k stage
+            atomicOr(&a.snz_n[(uint64_t)ct * a.nstw + (st >> 6)], 1ull << (st & 63u));
+        }
+        // (the next tile's first barrier orders sInc / sMisc reuse)
+    }
+    if (a.snap) {
+        snap_local = wave_sum(snap_local);
+        if (lane == 0 && snap_local) atomicAdd(a.snap, snap_local);
+    }
+    if (a.acct) {
+        const uint32_t tv[3] = {(uint32_t)wave_sum(t_srd), (uint32_t)wave_sum(t_swr), (uint32_t)wave_sum(t_fwr)};
+        if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < 3; q++)
+                if (tv[q]) acct_add(a.acct, 2 + q, (unsigned long long)tv[q]);
+        }
+        if (t == 0 && macs) acct_add(a.acct, 5, 2ull * kDenseTile * kDenseTile * kStageK * macs);
+        if (t == 0 && skipped) acct_add(a.acct, 6, skipped);
     }
 }

@@ -39,6 +39,7 @@
 #include <numeric>
 #include <queue>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <unordered_map>
 #include <vector>
@@ -55,6 +56,13 @@ namespace {
         if (_e != hipSuccess)                                                          \
             return set_error(GOSSIP_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
+
+// A collective being enqueued on an engine's communicator (COMM_TRY, gossip_engine_abort)
+struct CommIssue {
+    std::atomic<int>& c;
+    explicit CommIssue(std::atomic<int>& x) : c(x) { c.fetch_add(1); }
+    ~CommIssue() { c.fetch_sub(1); }
+};
 
 // Per-word control for one tick (host-built, uploaded each tick).
 struct WordCtl {
@@ -112,8 +120,6 @@ struct PullArgs {
     // counters are added and occupancy bits OR'ed atomically (nz_next zeroed beforehand)
     uint32_t shared_out = 0;
     uint32_t keep_lds = 0;  // some word of the launch has WF_KEEP: masks staged in LDS (k_pull)
-    // DENSE phase span (k_dense_dedup): every block ORs its end time (s_memrealtime) into [1]
-    unsigned long long* phase_ts = nullptr;
     uint32_t gate_seen = 1;  // k_pull<LPW,1>: skip the own-seen loads of tiles no peer occupies
     // Pass -> tile map (option pull_tiles): a k_pull pass covers LPW / 8 tiles taken from this
     // list of launch-local tile indices (0xffff = padding) instead of LPW / 8 consecutive tiles,
@@ -222,12 +228,13 @@ uint64_t pull_grid_cap(bool nt, int64_t ov) {
     return nt ? 16384ull : 4096ull;
 }
 
-// Word-lanes per node of the sparse pull for windows wider than 64 words.  32 lanes (passes of
-// 64 words, two nodes per wave step: twice the independent peer chains per wave, and a window
-// never ends in a half-idle 128-word pass) against 64 lanes, on the C4 / C3 benches
-// (profiles/r01/lanes_ab.json): C4 1216 words 127.7 -> 121.9 ms per launch, C4 8-shard 320 words
-// 44.0 -> 36.5 ms, C3 3.35 -> 3.06 ms; 16 lanes were slower on C4 (128.0 ms).
-int pull_lanes_per_node(int64_t ov) { return ov == 16 || ov == 32 || ov == 64 ? (int)ov : 32; }
+// Word-lanes per node of the sparse pull for windows wider than 64 words: 32 (passes of 64 words,
+// two nodes per wave step: twice the independent peer chains per wave, and a window never ends in
+// a half-idle 128-word pass).  Measured against 64 lanes (profiles/r01/lanes_ab.json: C4 1216
+// words 127.7 -> 121.9 ms per launch, the 8-shard 320 words 44.0 -> 36.5 ms, C3 3.35 -> 3.06 ms),
+// 16 lanes (C4 128.0 ms) and again in round 4 (64 lanes: C4 phase 69.0 vs 60.4 ms,
+// profiles/r04/ab/r4l_*); the option that selected them was removed in round 5.
+constexpr int kWideLanes = 32;
 
 template <int LPW, int EPN>
 void launch_pull_t(bool nt, uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
@@ -301,6 +308,11 @@ struct BirthArgs {
     uint16_t* list;            // young tiles: seen lists (young_kernel.h)
     const uint8_t* wt_yid;     // write-sparse index -> young id, this tick
     uint32_t list_max;         // entries a list holds (kListU16 - 1; option young_list_cap)
+    // fused DENSE tick (k_dense_fused): a birth also sets its bit in the transposed F_next and the
+    // (column tile, K stage) bit of its stage mask (null otherwise)
+    uint32_t* FTn = nullptr;
+    unsigned long long* snz_n = nullptr;
+    uint32_t kw = 0, nstw = 0;
 };
 
 // Seen-list entries [lo, hi] of node list ls in young id yid, word wit (bits of word w)
@@ -487,6 +499,11 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
         a.effgen[v] += 1u;
         atomicOr(&a.live[w], (unsigned long long)bit);
         if (a.snap && x.phase < a.snap_r) atomicAdd(a.snap, 1ull);
+        if (a.FTn) {
+            atomicOr(&a.FTn[(uint64_t)x.col * a.kw + (v >> 5)], 1u << (v & 31u));
+            const uint32_t st = (uint32_t)(v >> 10);  // 1,024-node K stage
+            atomicOr(&a.snz_n[(uint64_t)(x.col >> 8) * a.nstw + (st >> 6)], 1ull << (st & 63u));
+        }
     }
 }
 
@@ -529,12 +546,15 @@ __global__ __launch_bounds__(256) void k_sum_u32(const uint32_t* a, const uint32
     if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, s);
 }
 
-// One tick's DENSE phase span into ts[2] (ts[3] counts them); resets the start / end stamps.
+// The DENSE phase's device stamps (s_memrealtime, 100 MHz), one thread each, in stream order:
+// k_phase_start runs when the kernel before the phase has finished, k_phase_acc when the phase's
+// last kernel has, and adds the span to ts[2] (ts[3] counts them).  Round 4 stamped from every
+// block of the phase kernels with same-address atomics, which slowed k_transpose 6x.
+__global__ void k_phase_start(unsigned long long* ts) { ts[0] = __builtin_amdgcn_s_memrealtime(); }
 __global__ void k_phase_acc(unsigned long long* ts) {
-    if (ts[1] > ts[0] && ts[0] != ~0ull) ts[2] += ts[1] - ts[0];
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    if (now > ts[0]) ts[2] += now - ts[0];
     ts[3] += 1ull;
-    ts[0] = ~0ull;
-    ts[1] = 0ull;
 }
 
 // Σ sent = Σ (births' sends + deg x recv), the derived sent counter (header comment)
@@ -666,7 +686,16 @@ struct gossip_engine {
     bool dense = false;
     uint32_t n_pad = 0;
     uint32_t* d_Ab = nullptr;
-    uint32_t* d_FT = nullptr;
+    // the transposed frontier of F[0] / F[1]: k_transpose fills FT[fcur] (three-kernel path), or
+    // k_dense_fused + k_births fill FT[nxt] for the next tick (fused path, dense_kernel.h)
+    uint32_t* d_FT[2] = {nullptr, nullptr};
+    // fused path: per column tile (256 columns) and 1,024-node K stage, bit = FT holds a bit there;
+    // three buffers by tick: tick t reads [t % 3], writes [(t + 1) % 3] (with k_births), zeroes [(t + 2) % 3]
+    unsigned long long* d_snz[3] = {nullptr, nullptr, nullptr};
+    uint32_t snz_nstw = 0;              // mask words per column tile
+    bool ft_valid = false;              // d_FT[fcur] / d_snz[fcur] were written by the fused path
+    int64_t opt_dense_fused = 1;        // 1: k_dense_fused when the tick allows it (tick_step_a)
+    uint64_t fused_launches = 0;
     unsigned long long* d_inc = nullptr;  // n x stride incoming words (GEMM -> pull)
     uint32_t *d_recv = nullptr, *d_gen = nullptr, *d_effgen = nullptr;
     uint64_t* d_sent = nullptr;
@@ -693,14 +722,11 @@ struct gossip_engine {
     // ---- tuning options (gossip_engine_set_option; environment defaults)
     int64_t opt_pull_nt = -1;         // -1 = by live footprint (kPullNtBytes), 0/1 forced
     int64_t opt_pull_grid = 0;        // 0 = pull_grid_cap's default
-    int64_t opt_pull_lds_min = 0;     // k_pull launches reserve at least this much LDS per block
-                                      // (caps its blocks per CU, leaving CUs room for k_pull_young)
-    int64_t opt_pull_lpw = 0;         // 0 = 32 word-lanes for wide windows
     int64_t opt_dense_min_tiles = 512;  // block tiles the MFMA K split aims for
     int64_t opt_young = -1;           // young tiles (k_pull_young): -1 auto, 0 off, 1 on
     int64_t opt_young_age = 5;        // write-sparse while the oldest shares are <= this many hops
     int64_t opt_young_cap = 127;      // slot entries per node before it overflows to dense rows
-    int64_t opt_young_overlap = 1;    // k_pull_young beside k_pull on a second stream (1-4) or after (0)
+    int64_t opt_young_overlap = 1;    // k_pull_young beside k_pull on a second stream, launched first (1), or after it (0)
     int64_t opt_young_grid = 0;       // k_pull_young blocks, 0 = twice the pull grid (C4: 32,768 vs 16,384 blocks, -0.26 ms per phase over 3 same-box pairs, profiles/r04/ab/)
     int64_t opt_pull_gate = 1;        // k_pull: occupancy-gated own-seen loads
     int64_t opt_pull_tiles = 1;       // k_pull: passes over the listed (allocated, non-young) tiles only
@@ -720,6 +746,10 @@ struct gossip_engine {
     uint32_t tmask_cap = 0;                // words per slot
     bool sat_used = false;                 // this tick's k_pull keeps saturation bits
     std::vector<int64_t> tile_listed;      // last tick a tile was in k_pull's lists
+    // last tick k_pull wrote the tile's saturation bits (listed in a launch that kept them): the
+    // bits are trusted only the tick after, so turning pull_sat off and on again never trusts
+    // bits written before a tick that listed the tile without them
+    std::vector<int64_t> tile_satw;
     std::vector<int64_t> tile_dw;          // last tick every node's F_next row of the tile was written
     std::vector<int64_t> tile_inj_prev;    // the injection tick before tile_last_inject
     std::vector<uint32_t> tile_cols;       // columns allocated in the tile (this life)
@@ -761,6 +791,7 @@ struct gossip_engine {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers_young;
     double young_ms_done = 0.0;
     uint64_t young_launches = 0;
+    uint32_t last_young_grid = 0;
     // ---- timing / counters
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers;
     std::vector<hipEvent_t> event_pool;
@@ -787,7 +818,7 @@ struct gossip_engine {
     // compressed row exchange (row partition): message buffers and traffic counters
     int pack_rows(int64_t t, uint32_t c, hipStream_t s);
     int unpack_rows(int64_t t, uint32_t r, uint32_t c, const uint64_t* msg, uint64_t words, hipStream_t s);
-    int ensure_dev(uint64_t*& p, uint64_t& cap, uint64_t words);
+    int ensure_dev(uint64_t*& p, uint64_t& cap, uint64_t words, uint64_t preserve = 0);
     uint64_t* d_msg = nullptr;       // this rank's packed message
     uint64_t msg_cap = 0, msg_words = 0;
     uint32_t* d_cnt = nullptr;
@@ -813,6 +844,7 @@ struct gossip_engine {
                    uint64_t r0, uint64_t r1, bool prefix, hipStream_t s);
     uint64_t sizes_cap = 0;
     std::atomic<bool> aborted{false};  // gossip_engine_abort: comm torn down by another thread
+    std::atomic<int> comm_issuing{0};  // collectives being issued on comm right now (COMM_TRY)
     uint64_t exchange_bytes_out = 0, exchange_bytes_in = 0;
     bool tick_open = false;          // host-staged stepping: tick_begin done, tick_end pending
     // Pipelined exchange (option xchunks, row partition only): the own rows go through the pull
@@ -841,7 +873,7 @@ struct gossip_engine {
     struct RehearseEv { uint32_t range, kind; hipEvent_t a, b; };  // kind 0 pull, 1 pack, 2 unpack
     std::vector<RehearseEv> rr_events;
     std::vector<double> rr_ms[3];
-    std::vector<uint64_t> rr_bytes;
+    std::vector<uint64_t> rr_bytes, rr_bytes_max;
     uint64_t rr_ticks = 0;
     int rehearse_exchange(int64_t t);
     void rehearse_harvest();
@@ -869,7 +901,7 @@ gossip_engine::~gossip_engine() {
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
     hipFree(d_rowptr_c); hipFree(d_col_c); hipFree(d_degc);
     for (int k = 0; k < 4; k++) { hipFree(d_smask[k]); hipHostFree(h_smask[k]); }
-    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen_mem); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_sat); hipFree(d_Ab); hipFree(d_FT); hipFree(d_inc);
+    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen_mem); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_sat); hipFree(d_Ab); hipFree(d_FT[0]); hipFree(d_FT[1]); hipFree(d_snz[0]); hipFree(d_snz[1]); hipFree(d_snz[2]); hipFree(d_inc);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent); hipFree(d_phase_ts);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     hipFree(d_msg); hipFree(d_cnt); hipFree(d_scan_tmp); hipFree(d_recv_msgs); hipFree(d_sizes);
@@ -975,11 +1007,19 @@ int gossip_engine::prepare_instances() {
         const uint32_t ns = (uint32_t)(e - k);
         if (ns > 64)
             return set_error(GOSSIP_EINVAL, "more than 64 generations share one id in one component");
-        // Same rule as gossip_shard_events (host.cpp): lone ids by (id, node), others by
-        // (id, component).
-        const uint64_t hkey = lone ? gossip::instance_hash(keys[k].id, ev[keys[k].ev].node, true)
-                                   : gossip::instance_hash(keys[k].id, keys[k].comp, false);
-        const bool mine = S == 1 || (hkey % S) == cfg.shard_rank;
+        // Same rules as gossip_shard_events / _by_tick (host.cpp): lone ids by (id, node), others
+        // by (id, component); hashed, or (GOSSIP_F_SHARD_BY_TICK) by the tick of the instance's
+        // first generation
+        bool mine = S == 1;
+        if (!mine && (cfg.flags & GOSSIP_F_SHARD_BY_TICK)) {
+            int64_t first = keys[k].ns;
+            for (uint64_t q = k + 1; q < e; q++) first = std::min(first, keys[q].ns);
+            mine = (uint64_t)(first / L) % S == cfg.shard_rank;
+        } else if (!mine) {
+            const uint64_t hkey = lone ? gossip::instance_hash(keys[k].id, ev[keys[k].ev].node, true)
+                                       : gossip::instance_hash(keys[k].id, keys[k].comp, false);
+            mine = (hkey % S) == cfg.shard_rank;
+        }
         if (!mine) {
             for (uint64_t q = k; q < e; q++) keep[keys[q].ev] = 0;
         } else {
@@ -1132,7 +1172,7 @@ int gossip_engine::alloc_device() {
         const uint64_t want = stride + std::max<uint64_t>(stride / 4, 2 * kTileWords);
         const uint64_t other = (uint64_t)n * 24 + nnz * 4 + ((uint64_t)n + 1) * 8 + slot_bytes +
                                24ull * n * ((want + 1023u) / 1024u) + (4ull << 30);  // + RCCL / context (24: nz x 2 + sat)
-        const uint64_t per_word = 3ull * n * 8 + (dense ? 8ull * n_pad : 0ull);
+        const uint64_t per_word = 3ull * n * 8 + (dense ? 16ull * n_pad : 0ull);  // (DENSE: FT x 2)
         uint64_t fit = freeb > other ? ((uint64_t)freeb - other) / per_word : 0ull;
         fit = fit / kTileWords * kTileWords;
         stride = (uint32_t)std::max<uint64_t>(stride, std::min<uint64_t>(want / kTileWords * kTileWords, fit));
@@ -1272,11 +1312,20 @@ int gossip_engine::alloc_device() {
                    kRing * ((uint64_t)stride * sizeof(WordCtl) + (uint64_t)bcap * sizeof(Birth) + pcap * 4);
     if (dense) {
         const uint64_t ft = (uint64_t)stride * 8 * n_pad;
-        HIP_TRY(hipMalloc(&d_FT, ft));
-        HIP_TRY(hipMemsetAsync(d_FT, 0, ft, stream));
+        snz_nstw = (n_pad / kStageK + 63u) / 64u;
+        const uint64_t snzb = (uint64_t)(stride / 4u) * snz_nstw * 8u;
+        for (int k = 0; k < 3; k++) {
+            if (k < 2) {
+                HIP_TRY(hipMalloc(&d_FT[k], ft));
+                HIP_TRY(hipMemsetAsync(d_FT[k], 0, ft, stream));
+            }
+            HIP_TRY(hipMalloc(&d_snz[k], snzb));
+            HIP_TRY(hipMemsetAsync(d_snz[k], 0, snzb, stream));
+        }
+        ft_valid = false;
         HIP_TRY(hipMalloc(&d_inc, bm));
         HIP_TRY(hipMemsetAsync(d_inc, 0, bm, stream));
-        device_bytes += ft + bm + (uint64_t)n_pad * n_pad / 8;
+        device_bytes += 2 * ft + 3 * snzb + bm + (uint64_t)n_pad * n_pad / 8;
     }
     if (batch && !snaps.empty())
         for (int k = 0; k < kRing; k++) {
@@ -1291,6 +1340,7 @@ int gossip_engine::alloc_device() {
     tile_widx.assign(stride / kTileWords, 0xffu);
     tile_yid.assign(stride / kTileWords, (uint8_t)kYidNone);
     tile_listed.assign(stride / kTileWords, INT64_MIN);
+    tile_satw.assign(stride / kTileWords, INT64_MIN);
     tile_dw.assign(stride / kTileWords, INT64_MIN);
     tile_inj_prev.assign(stride / kTileWords, INT64_MIN);
     tile_cols.assign(stride / kTileWords, 0u);
@@ -1316,9 +1366,12 @@ int gossip_engine::grow(uint32_t new_stride) {
         // exchange.
         int* d_ok = reinterpret_cast<int*>(d_scalars);  // scratch word [0]
         HIP_TRY(hipMemcpyAsync(d_ok, &ok, sizeof(int), hipMemcpyHostToDevice, stream));
-        if (aborted.load()) return set_error(GOSSIP_ESTATE, "RCCL: the row partition was aborted");
-        if (ncclAllReduce(d_ok, d_ok, 1, ncclInt32, ncclMin, comm, stream) != ncclSuccess)
-            return set_error(GOSSIP_EHIP, "RCCL: capacity agreement failed");
+        {
+            CommIssue issuing_(comm_issuing);
+            if (aborted.load()) return set_error(GOSSIP_ESTATE, "RCCL: the row partition was aborted");
+            if (ncclAllReduce(d_ok, d_ok, 1, ncclInt32, ncclMin, comm, stream) != ncclSuccess)
+                return set_error(GOSSIP_EHIP, "RCCL: capacity agreement failed");
+        }
         HIP_TRY(hipMemcpyAsync(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
     }
@@ -1391,17 +1444,27 @@ int gossip_engine::grow(uint32_t new_stride) {
         if (!rc) rc = regrow_host(h_live[k], 8, stride, new_stride);
     }
     if (rc) return rc;
-    if (dense) {  // transposed frontier and incoming words are rebuilt every tick: no copy
-        HIP_TRY(hipFree(d_FT));
-        HIP_TRY(hipFree(d_inc));
-        d_FT = nullptr;
-        d_inc = nullptr;
+    if (dense) {  // transposed frontier and incoming words: rebuilt (k_transpose next tick), no copy
         const uint64_t ft = (uint64_t)new_stride * 8 * n_pad;
-        HIP_TRY(hipMalloc(&d_FT, ft));
-        HIP_TRY(hipMemset(d_FT, 0, ft));
+        const uint64_t snzb = (uint64_t)(new_stride / 4u) * snz_nstw * 8u;
+        for (int k = 0; k < 3; k++) {
+            if (k < 2) {
+                HIP_TRY(hipFree(d_FT[k]));
+                d_FT[k] = nullptr;
+                HIP_TRY(hipMalloc(&d_FT[k], ft));
+                HIP_TRY(hipMemset(d_FT[k], 0, ft));
+            }
+            HIP_TRY(hipFree(d_snz[k]));
+            d_snz[k] = nullptr;
+            HIP_TRY(hipMalloc(&d_snz[k], snzb));
+            HIP_TRY(hipMemset(d_snz[k], 0, snzb));
+        }
+        ft_valid = false;
+        HIP_TRY(hipFree(d_inc));
+        d_inc = nullptr;
         HIP_TRY(hipMalloc(&d_inc, nb));
         HIP_TRY(hipMemset(d_inc, 0, nb));
-        device_bytes += (uint64_t)(new_stride - stride) * (8ull * n_pad + 8ull * n);
+        device_bytes += (uint64_t)(new_stride - stride) * (16ull * n_pad + 8ull * n + 6ull * snz_nstw);
     }
     if (batch && !snaps.empty())
         for (int k = 0; k < kRing; k++) {  // rebuilt every tick: no copy
@@ -1416,6 +1479,7 @@ int gossip_engine::grow(uint32_t new_stride) {
     tile_last_inject.resize(new_stride / kTileWords, INT64_MIN);
     tile_first.resize(new_stride / kTileWords, INT64_MIN);
     tile_listed.resize(new_stride / kTileWords, INT64_MIN);
+    tile_satw.resize(new_stride / kTileWords, INT64_MIN);
     tile_dw.resize(new_stride / kTileWords, INT64_MIN);
     tile_inj_prev.resize(new_stride / kTileWords, INT64_MIN);
     tile_cols.resize(new_stride / kTileWords, 0u);
@@ -1469,6 +1533,7 @@ int gossip_engine::alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t
         tile_first[tl] = t;
         tile_cols[tl] = 0;  // (a new life: nothing of the previous one is trusted)
         tile_listed[tl] = INT64_MIN;
+        tile_satw[tl] = INT64_MIN;
         tile_dw[tl] = INT64_MIN;
         for (uint32_t q = 0; q < kTileWords; q++) reset_now.push_back(tl * kTileWords + q);
         open_tile = tl;
@@ -1739,6 +1804,7 @@ int gossip_engine::tick_step_a(int64_t t) {
     bool smask_any = false;
     if (nsnap && hw) std::memset(h_smask[slot], 0, (size_t)nsnap * hw * 8);
     bool keep_any = false;  // some word has a keep mask (k_pull stages them in LDS)
+    bool group_any = false; // some word holds an id group (k_dense_fused leaves those ticks to the 3-kernel path)
     for (uint32_t w = 0; w < hw; w++) {
         WordCtl c = ctl[w];
         if (batch) {
@@ -1776,6 +1842,7 @@ int gossip_engine::tick_step_a(int64_t t) {
         WF[w] = (uint8_t)((c.clear ? WF_CLEAR : 0u) | (c.gmask ? WF_GROUP : 0u) |
                           (c.keep != ~0ull ? WF_KEEP : 0u) | (c.snap ? WF_SNAP : 0u));
         keep_any |= c.keep != ~0ull;
+        group_any |= c.gmask != 0ull;
     }
     if (const int64_t late = late_age_now())  // bottom-up early exit in k_pull (tiles >= late ticks old)
         for (uint32_t w = 0; w < hw; w++) {
@@ -1794,7 +1861,7 @@ int gossip_engine::tick_step_a(int64_t t) {
     pt_cnt.clear();
     const bool use_ptile = opt_pull_tiles && !dense && !(cfg.flags & GOSSIP_F_NOSKIP) && hw;
     pt_used = use_ptile;
-    const bool sat_on = use_ptile && opt_pull_sat != 0 && !(cfg.flags & GOSSIP_F_NOSKIP) && d_sat;
+    const bool sat_on = use_ptile && opt_pull_sat != 0 && row_count == 1 && !(cfg.flags & GOSSIP_F_NOSKIP) && d_sat;
     const bool dr_used = use_ptile && opt_dense_rows != 0 && row_count == 1 && !(cfg.flags & GOSSIP_F_NOSKIP);
     if (use_ptile) {
         const uint64_t need = (uint64_t)hw / kTileWords + 16ull * ((hw + kPullLdsWords - 1) / kPullLdsWords) + 16;
@@ -1814,7 +1881,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             const uint32_t wl = std::min(kPullLdsWords, hw - wb);
             int lpw = 8;
             while (lpw < 64 && 2 * lpw < (int)wl) lpw *= 2;
-            if (lpw == 64) lpw = pull_lanes_per_node(opt_pull_lpw);  // (run_pull: wide windows)
+            if (lpw == 64) lpw = kWideLanes;  // (run_pull: wide windows)
             const uint32_t tpp = (uint32_t)lpw / 8u;
             pt_off.push_back(at);
             const uint32_t t0 = wb / kTileWords, t1 = (wb + wl) / kTileWords;
@@ -1881,7 +1948,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             m[dr ? TM_DENSE : TM_NZ] |= bit;
             // sat bits written by k_pull last tick, no birth since
             const bool clean = !fresh && tile_last_inject[tl] != t - 1 && tile_inj_prev[tl] != t - 1;
-            if (sat_used && clean && tile_listed[tl] == t - 1) m[TM_SATOK] |= bit;
+            if (sat_used && clean && tile_satw[tl] == t - 1) m[TM_SATOK] |= bit;
             if (dr_used && dense_row_hop(tl, t - tile_first[tl])) {  // F_cur's hop next tick
                 for (uint32_t q = 0; q < kTileWords; q++) WF[tl * kTileWords + q] |= (uint8_t)WF_DW;
                 tile_dw[tl] = t;
@@ -1911,6 +1978,10 @@ int gossip_engine::tick_step_a(int64_t t) {
     if (wact) HIP_TRY(hipMemsetAsync(d_live[lv], 0, (size_t)wact * 8, stream));
     unsigned long long* snap_ptr = snap_idx >= 0 ? d_scalars + 2 + 2 * snap_idx + 1 : nullptr;
     const int nxt = fcur ^ 1;
+    // DENSE ticks run k_dense_fused (dense_kernel.h) unless the tick has id groups, row chunks
+    // (row partition: other ranks' rows reach F_next without FT), or the diagnostic no-skip pull
+    const bool fused_tick = dense && wact && opt_dense_fused && nchunks == 1 && row_count == 1 &&
+                            !(cfg.flags & GOSSIP_F_NOSKIP) && !group_any;
     // births [off, off + cnt) of the staged array (all of them, or one row chunk's)
     auto launch_births = [&](uint32_t off, uint32_t cnt) -> int {
         if (!cnt) return GOSSIP_OK;
@@ -1932,6 +2003,12 @@ int gossip_engine::tick_step_a(int64_t t) {
         b.list = d_ylist;
         b.list_max = (uint32_t)opt_young_list_cap;
         b.wt_yid = young ? d_young[slot]->wt_yid : nullptr;
+        if (fused_tick) {
+            b.FTn = d_FT[nxt];
+            b.snz_n = d_snz[(t + 1) % 3];
+            b.kw = n_pad / 32u;
+            b.nstw = snz_nstw;
+        }
         k_births<<<(cnt + 255) / 256, 256, 0, stream>>>(b);
         HIP_TRY(hipGetLastError());
         return GOSSIP_OK;
@@ -1992,7 +2069,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 while (lpw < 64 && 2 * lpw < (int)c.wact) lpw *= 2;
                 // windows wider than 64 words keep one peer walk per node (the pipelined path)
                 const bool wide_window = lpw == 64 && split_edges;
-                if (wide_window) lpw = pull_lanes_per_node(opt_pull_lpw);
+                if (wide_window) lpw = kWideLanes;
                 int epn = 1;
                 while (split_edges && !wide_window && lpw * epn * 2 <= 64 && epn * 8 < avg_deg) epn *= 2;
                 // saturation bits / dense-row tiles: the gathering kernel (EPN 1) over tile lists
@@ -2002,10 +2079,12 @@ int gossip_engine::tick_step_a(int64_t t) {
                     c.sat = sat_used ? d_sat : nullptr;
                     extra_lds = kPullSatLds;
                     sat_launches += sat_used;
+                    if (sat_used)  // this launch writes the sat bits of its listed tiles
+                        for (uint32_t tl = wb / kTileWords; tl < (wb + c.wact) / kTileWords; tl++)
+                            if (tile_listed[tl] == t) tile_satw[tl] = t;
                 }
                 last_lpw = (uint32_t)lpw;
-                const size_t lds = std::max<size_t>(pull_lds_bytes(c.wact, c.keep_lds != 0, c.nptile) + extra_lds,
-                                                    (size_t)opt_pull_lds_min);
+                const size_t lds = pull_lds_bytes(c.wact, c.keep_lds != 0, c.nptile) + extra_lds;
                 launch_pull(lpw, epn, nt_rows, grid, lds, stream, c);
             }
         };
@@ -2013,16 +2092,20 @@ int gossip_engine::tick_step_a(int64_t t) {
         a.inc = nullptr;
         // DENSE phase = transpose + MFMA + dedup, timed as ONE unit (below)
         const bool dense_timing = dense && (cfg.flags & GOSSIP_F_TIMING);
-        // The DENSE phase is timed on the device: the first k_transpose block's start and the last
-        // k_dense_dedup block's end (s_memrealtime, 100 MHz), accumulated per tick by
-        // k_phase_acc -- the span a kernel trace shows.  An event pair around the phase also
-        // counted the host's launch latency: 273 us against a 136 us span on C2 (profiles/r04).
+        // The DENSE phase is timed on the device by two one-thread stamp kernels around it
+        // (k_phase_start, k_phase_acc): an event pair around the phase also counted the host's
+        // launch latency (273 us against a 136 us span on C2, profiles/r04).
         unsigned long long* pts = dense_timing ? d_phase_ts : nullptr;
-        a.phase_ts = pts;
-        if (dense) {  // transpose the frontier to share-column bit rows (not timed as the pull)
+        // a fused tick after a three-kernel one: the stage masks it writes were not zeroed
+        if (fused_tick && !ft_valid)
+            HIP_TRY(hipMemsetAsync(d_snz[(t + 1) % 3], 0, (size_t)(stride / 4u) * snz_nstw * 8u, stream));
+        if (pts) k_phase_start<<<1, 1, 0, stream>>>(pts);
+        if (dense && !(fused_tick && ft_valid)) {
+            // transpose the frontier to share-column bit rows (the fused path's FT[fcur] was
+            // written by the last tick's k_dense_fused + k_births)
             dim3 eg(n_pad / 256u, wact);
             k_transpose<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad / 32u, wact, a.live_prev,
-                                                d_nz[fcur], ntw, d_FT, pts);
+                                                d_nz[fcur], ntw, d_FT[fcur]);
             HIP_TRY(hipGetLastError());
         }
         // young tiles beside k_pull: the two kernels touch disjoint words; they share the per-node
@@ -2031,11 +2114,9 @@ int gossip_engine::tick_step_a(int64_t t) {
         const bool overlap = !dense && ny && opt_young_overlap != 0;
         if (overlap) {
             if (!ystream) {
-                // young_overlap 3 / 4: the second stream at the lowest / highest priority
-                int lo = 0, hi = 0;
-                HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-                const int prio = opt_young_overlap == 3 ? lo : opt_young_overlap == 4 ? hi : 0;
-                HIP_TRY(hipStreamCreateWithPriority(&ystream, hipStreamNonBlocking, prio));
+                // (launch order, stream priorities and smaller young grids measured no better:
+                // profiles/r02, r03/ab/r3v_*; those variants were removed in round 5)
+                HIP_TRY(hipStreamCreateWithFlags(&ystream, hipStreamNonBlocking));
                 HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
                 HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
             }
@@ -2083,6 +2164,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 y1 = get_event();
                 HIP_TRY(hipEventRecord(y0, ys));
             }
+            last_young_grid = yg;
             k_pull_young<<<yg, 256, young_lds_bytes(ny, ny_read), ys>>>(y);
             HIP_TRY(hipGetLastError());
             if (cfg.flags & GOSSIP_F_TIMING) {
@@ -2108,7 +2190,7 @@ int gossip_engine::tick_step_a(int64_t t) {
         // the MFMA contraction of rows [lo, hi) (DENSE mode) into the incoming words
         auto run_dense = [&](uint64_t lo, uint64_t hi) -> int {
             BitsArgs gm;
-            gm.Ab = d_Ab; gm.FT = d_FT; gm.inc = d_inc; gm.live_prev = a.live_prev; gm.acct = d_acct;
+            gm.Ab = d_Ab; gm.FT = d_FT[fcur]; gm.inc = d_inc; gm.live_prev = a.live_prev; gm.acct = d_acct;
             gm.n = (uint32_t)hi; gm.n_pad = n_pad; gm.kw = n_pad / 32u; gm.stride = stride;
             gm.mb0 = (uint32_t)lo / kDenseTile;  // row partition: this engine's row blocks only
             gm.mb = (std::min((uint32_t)hi + kDenseTile - 1u, n_pad) - (uint32_t)lo) / kDenseTile;
@@ -2155,6 +2237,31 @@ int gossip_engine::tick_step_a(int64_t t) {
                 if ((rc = end_chunk(c))) return rc;
             }
             if (pts) k_phase_acc<<<1, 1, 0, stream>>>(pts);  // (row chunks: the chunks' births are inside the span)
+        } else if (fused_tick) {
+            // the whole DENSE pull in one persistent kernel (contraction, dedup, FT of F_next)
+            FusedArgs f;
+            f.Ab = d_Ab; f.FTc = d_FT[fcur]; f.FTn = d_FT[nxt];
+            f.snz_c = ft_valid ? d_snz[t % 3] : nullptr;
+            f.snz_n = d_snz[(t + 1) % 3];
+            f.snz_z = d_snz[(t + 2) % 3];
+            f.snz_zwords = (stride / 4u) * snz_nstw;
+            f.seen = d_seen; f.Fnext = d_F[nxt]; f.ctl = d_ctl[slot]; f.wflags = d_wflags[slot];
+            f.recv = d_recv; f.live = d_live[lv]; f.live_prev = a.live_prev; f.snap = snap_ptr; f.acct = d_acct;
+            f.nz_next = d_nz[nxt]; f.ntw = ntw;
+            f.n = n; f.n_pad = n_pad; f.kw = n_pad / 32u; f.stride = stride;
+            f.nst = n_pad / kStageK; f.nstw = snz_nstw;
+            f.mb = n_pad / kDenseTile; f.nt = wact / 4u; f.total = f.mb * f.nt;
+            f.wact = wact;
+            uint32_t fg = (uint32_t)std::min<uint64_t>(f.total, (uint64_t)num_cus);
+            if (fg >= 8u) fg &= ~7u;
+            k_dense_fused<<<fg, 512, 0, stream>>>(f);
+            HIP_TRY(hipGetLastError());
+            fused_launches++;
+            if (cfg.flags & GOSSIP_F_TIMING) {
+                HIP_TRY(hipEventRecord(e1, stream));
+                timers.emplace_back(e0, e1);
+            }
+            if (pts) k_phase_acc<<<1, 1, 0, stream>>>(pts);
         } else if (dense) {
             // The timed kernel in DENSE mode is the MFMA contraction (pull_ms); its incoming
             // words are then consumed by k_dense_dedup.  The whole phase -- transpose, MFMA,
@@ -2195,19 +2302,13 @@ int gossip_engine::tick_step_a(int64_t t) {
             if (overlap) {
                 HIP_TRY(hipEventRecord(ev_fork, stream));
                 HIP_TRY(hipStreamWaitEvent(ystream, ev_fork, 0));
-                if (opt_young_overlap != 2) {
-                    const int rc = launch_young(ystream);
-                    if (rc) return rc;
-                }
+                const int rc = launch_young(ystream);
+                if (rc) return rc;
             }
             run_pull(a, true);
             if (cfg.flags & GOSSIP_F_TIMING) {
                 HIP_TRY(hipEventRecord(e1, stream));
                 timers.emplace_back(e0, e1);
-            }
-            if (overlap && opt_young_overlap == 2) {
-                const int rc = launch_young(ystream);
-                if (rc) return rc;
             }
             if (overlap) {
                 HIP_TRY(hipEventRecord(ev_join, ystream));
@@ -2247,6 +2348,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             HIP_TRY(hipGetLastError());
         }
     }
+    ft_valid = fused_tick;  // FT[nxt] / d_snz[(t + 1) % 3] describe the next tick's F_cur
     return GOSSIP_OK;
 }
 
@@ -2383,9 +2485,14 @@ DevLayout dev_layout(uint64_t k, uint32_t ntw, uint32_t wlive) {
     } while (0)
 // A collective on the engine's communicator (member functions): never after gossip_engine_abort
 // freed it (another thread's abort of a failing partition), whose later calls would use freed
-// memory -- the engine then reports GOSSIP_ESTATE.
+// memory -- the engine then reports GOSSIP_ESTATE.  The issue is bracketed by comm_issuing, and
+// gossip_engine_abort raises `aborted` first and then waits for comm_issuing == 0 before it frees
+// the communicator (both sequentially consistent): a call that saw `aborted` clear finishes
+// enqueueing before the abort, a later one sees it set.  (Enqueueing never waits for the peers.)
+// CommIssue is defined at the top of the file.
 #define COMM_TRY(x)                                                                         \
     do {                                                                                    \
+        CommIssue issuing_(comm_issuing);                                                   \
         if (aborted.load()) return set_error(GOSSIP_ESTATE, "RCCL: the row partition was aborted"); \
         NCCL_TRY(x);                                                                        \
     } while (0)
@@ -2394,22 +2501,30 @@ DevLayout dev_layout(uint64_t k, uint32_t ntw, uint32_t wlive) {
 // device_bytes (the engine's footprint, gossip_counters) and fail cleanly with GOSSIP_ENOMEM --
 // the callers' cue to split the shares into more shards -- when the device or the mem_limit
 // option has no room left, instead of a HIP error mid-run.
-int gossip_engine::ensure_dev(uint64_t*& p, uint64_t& cap, uint64_t words) {
+// preserve > 0: the first `preserve` words of the old buffer are copied into the new one (the old
+// buffer is then freed only after the copy, so the room check counts both).
+int gossip_engine::ensure_dev(uint64_t*& p, uint64_t& cap, uint64_t words, uint64_t preserve) {
     if (words <= cap) return GOSSIP_OK;
     HIP_TRY(hipStreamSynchronize(stream));  // (rare: growth) both streams may still read p
     if (xstream) HIP_TRY(hipStreamSynchronize(xstream));
     const uint64_t ncap = std::max<uint64_t>(words, cap + cap / 2);
     size_t freeb = 0, totalb = 0;
     HIP_TRY(hipMemGetInfo(&freeb, &totalb));
-    const uint64_t room = (uint64_t)freeb + cap * 8;  // (the old buffer is freed first)
+    const uint64_t room = (uint64_t)freeb + (preserve ? 0 : cap * 8);  // (without a copy the old buffer is freed first)
     if (ncap * 8 > room || (opt_mem_limit > 0 && device_bytes + (ncap - cap) * 8 > (uint64_t)opt_mem_limit))
         return set_error(GOSSIP_ENOMEM, "row exchange: no device memory for a " + std::to_string(ncap * 8) +
                                             "-byte message buffer (" + std::to_string(device_bytes) + " bytes held)");
+    uint64_t* q = nullptr;
+    if (preserve) {
+        HIP_TRY(hipMalloc(&q, ncap * 8));
+        HIP_TRY(hipMemcpy(q, p, std::min(preserve, cap) * 8, hipMemcpyDeviceToDevice));
+    }
     hipFree(p);
     p = nullptr;
     device_bytes -= cap * 8;
     cap = 0;
-    HIP_TRY(hipMalloc(&p, ncap * 8));
+    if (!preserve) HIP_TRY(hipMalloc(&q, ncap * 8));
+    p = q;
     cap = ncap;
     device_bytes += cap * 8;
     return GOSSIP_OK;
@@ -2453,15 +2568,10 @@ int gossip_engine::pack_range(int64_t t, uint64_t lo, uint64_t hi, uint32_t wliv
     HIP_TRY(hipMemcpyAsync(&total, off + k, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     const PackLayout L = pack_layout(k, ntw, total, wlive);
-    // (the layout's header parts do not depend on the row count: grow keeping them)
+    // (the layout's header parts do not depend on the row count: grow keeping them; through
+    // ensure_dev, so the growth counts in device_bytes and respects mem_limit)
     if (L.total > msg_cap) {
-        uint64_t* nm = nullptr;
-        HIP_TRY(hipMalloc(&nm, L.total * 8));
-        HIP_TRY(hipMemcpyAsync(nm, d_msg, L.rows * 8, hipMemcpyDeviceToDevice, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        hipFree(d_msg);
-        d_msg = nm;
-        msg_cap = L.total;
+        if ((rc = ensure_dev(d_msg, msg_cap, L.total, L.rows))) return rc;
         off = reinterpret_cast<uint32_t*>(d_msg + L.off);
     }
     const unsigned long long hdr = total;
@@ -2522,6 +2632,7 @@ int gossip_engine::rehearse_exchange(int64_t t) {
     const bool timing = (cfg.flags & GOSSIP_F_TIMING) != 0;
     const uint32_t R = (uint32_t)rr_lo.size() - 1;
     if (rr_bytes.size() != R) rr_bytes.assign(R, 0);
+    if (rr_bytes_max.size() != R) rr_bytes_max.assign(R, 0);
     for (uint32_t r = 0; r < R; r++) {
         const uint64_t lo = rr_lo[r], hi = rr_lo[r + 1];
         if (hi <= lo) continue;
@@ -2534,6 +2645,7 @@ int gossip_engine::rehearse_exchange(int64_t t) {
             rr_events.push_back({r, 1u, a, b});
         }
         rr_bytes[r] += msg_words * 8;
+        rr_bytes_max[r] = std::max<uint64_t>(rr_bytes_max[r], msg_words * 8);
         hipEvent_t c = timing ? get_event() : nullptr, d = timing ? get_event() : nullptr;
         if (timing) HIP_TRY(hipEventRecord(c, stream));
         if ((rc = unpack_range(t, lo, hi, hw, d_msg, msg_words, stream))) return rc;
@@ -2869,9 +2981,8 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->cur = e->tick0;
         e->opt_pull_nt = env_option("GOSSIP_PULL_NT", -1);
         e->opt_pull_grid = env_option("GOSSIP_PULL_GRID", 0);
-        e->opt_pull_lds_min = env_option("GOSSIP_PULL_LDS_MIN", 0);
-        e->opt_pull_lpw = env_option("GOSSIP_PULL_LPW", 0);
         e->opt_dense_min_tiles = env_option("GOSSIP_DENSE_MIN_TILES", 512);
+        e->opt_dense_fused = env_option("GOSSIP_DENSE_FUSED", 1);
         e->opt_young = env_option("GOSSIP_YOUNG", -1);
         e->opt_young_age = env_option("GOSSIP_YOUNG_AGE", 5);
         e->opt_young_cap = env_option("GOSSIP_YOUNG_CAP", 127);
@@ -3060,8 +3171,12 @@ int gossip_rccl_unique_id(uint8_t* out, uint32_t len) {
 int gossip_engine_abort(gossip_engine* e) {
     if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
     bool expected = false;
-    // (the flag first: the engine's own thread checks it before every collective, COMM_TRY)
-    if (e->aborted.compare_exchange_strong(expected, true) && e->comm) ncclCommAbort(e->comm);
+    // the flag first: the engine's own thread checks it before every collective (COMM_TRY); then
+    // wait until no collective is being enqueued on the communicator, and free it
+    if (e->aborted.compare_exchange_strong(expected, true) && e->comm) {
+        while (e->comm_issuing.load() != 0) std::this_thread::yield();
+        ncclCommAbort(e->comm);
+    }
     return GOSSIP_OK;
 }
 
@@ -3192,16 +3307,9 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     if (k == "pull_nt") {
         if (value < -1 || value > 1) return set_error(GOSSIP_EINVAL, "pull_nt: -1 (auto), 0 or 1");
         e->opt_pull_nt = value;
-    } else if (k == "pull_lds_min") {
-        if (value < 0 || value > 160 * 1024) return set_error(GOSSIP_EINVAL, "pull_lds_min: 0 .. 163840 bytes");
-        e->opt_pull_lds_min = value;
     } else if (k == "pull_grid") {
         if (value < 0 || value > (1ll << 24)) return set_error(GOSSIP_EINVAL, "pull_grid: 0 (auto) .. 2^24 blocks");
         e->opt_pull_grid = value;
-    } else if (k == "pull_lpw") {
-        if (value != 0 && value != 16 && value != 32 && value != 64)
-            return set_error(GOSSIP_EINVAL, "pull_lpw: 0 (auto), 16, 32 or 64");
-        e->opt_pull_lpw = value;
     } else if (k == "young") {
         if (value < -1 || value > 1) return set_error(GOSSIP_EINVAL, "young: -1 (auto), 0 or 1");
         if (e->have_sched) return set_error(GOSSIP_ESTATE, "young: set before the schedule");
@@ -3213,7 +3321,7 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
         if (value < 1 || value > (int64_t)kSlotU16 - 1) return set_error(GOSSIP_EINVAL, "young_cap: 1 .. 127 entries");
         e->opt_young_cap = value;
     } else if (k == "young_overlap") {
-        if (value < 0 || value > 4) return set_error(GOSSIP_EINVAL, "young_overlap: 0 .. 4");
+        if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "young_overlap: 0 or 1");
         e->opt_young_overlap = value;
     } else if (k == "pull_tile_order") {
         if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "pull_tile_order: 0 or 1");
@@ -3257,6 +3365,9 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
         if (value > 1 && e->row_count > 1)
             return set_error(GOSSIP_EINVAL, "rehearse_rows: an unpartitioned CSR engine");
         e->opt_rehearse_rows = value;
+    } else if (k == "dense_fused") {
+        if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "dense_fused: 0 or 1");
+        e->opt_dense_fused = value;
     } else if (k == "dense_min_tiles") {
         if (value < 1) return set_error(GOSSIP_EINVAL, "dense_min_tiles >= 1");
         e->opt_dense_min_tiles = value;
@@ -3264,6 +3375,27 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
         return set_error(GOSSIP_EINVAL, "unknown option '" + k + "'");
     }
     return GOSSIP_OK;
+}
+
+int gossip_engine_get_option(const gossip_engine* e, const char* name, int64_t* value) {
+    if (!e || !name || !value) return set_error(GOSSIP_EINVAL, "NULL argument");
+    const std::string k(name);
+    const std::pair<const char*, int64_t> opts[] = {
+        {"pull_nt", e->opt_pull_nt}, {"pull_grid", e->opt_pull_grid},
+        {"young", e->opt_young}, {"young_age", e->opt_young_age},
+        {"young_cap", e->opt_young_cap}, {"young_overlap", e->opt_young_overlap},
+        {"pull_tile_order", e->opt_pull_tile_order}, {"pull_tiles", e->opt_pull_tiles},
+        {"pull_sat", e->opt_pull_sat}, {"dense_rows", e->opt_dense_rows}, {"pull_gate", e->opt_pull_gate},
+        {"young_list_cap", e->opt_young_list_cap}, {"young_nt", e->opt_young_nt},
+        {"young_grid", e->opt_young_grid}, {"mem_limit", e->opt_mem_limit}, {"late_age", e->opt_late_age},
+        {"xchunks", e->opt_xchunks}, {"rehearse_rows", e->opt_rehearse_rows},
+        {"dense_fused", e->opt_dense_fused}, {"dense_min_tiles", e->opt_dense_min_tiles}};
+    for (const auto& o : opts)
+        if (k == o.first) {
+            *value = o.second;
+            return GOSSIP_OK;
+        }
+    return set_error(GOSSIP_EINVAL, "unknown option '" + k + "'");
 }
 
 // Host-staged exchange (any transport): tick_begin -> export own message -> import every other
@@ -3718,7 +3850,7 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     c->young_fresh_lines = acct[19];
 #ifdef YOUNG_STAMPS
     fprintf(stderr, "young_stamps_cycles");
-    for (int k = 20; k < 28; k++) fprintf(stderr, " %llu", (unsigned long long)acct[k]);
+    for (int k = 22; k < 30; k++) fprintf(stderr, " %llu", (unsigned long long)acct[k]);  // (20, 21: k_pull items)
     fprintf(stderr, "\n");
 #endif
     c->young_list_lines = acct[17] + acct[18];
@@ -3727,6 +3859,8 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     c->pull_sat_skips = acct[16];
     c->pull_items = acct[20];
     c->pull_gather_items = acct[21];
+    c->dense_fused_launches = e->fused_launches;
+    c->young_grid = e->last_young_grid;
     c->pull_sat = e->sat_used ? 1u : 0u;
     c->window_early_retires = e->early_retires;
     uint64_t g = 0;
@@ -3751,6 +3885,14 @@ int gossip_engine_get_rehearsal(gossip_engine* e, uint32_t ranges, double* pull_
         if (msg_bytes) msg_bytes[r] = r < e->rr_bytes.size() ? e->rr_bytes[r] : 0;
     }
     if (ticks) *ticks = e->rr_ticks;
+    return GOSSIP_OK;
+}
+
+int gossip_engine_get_rehearsal_peak(gossip_engine* e, uint32_t ranges, uint64_t* msg_bytes_max) {
+    if (!e || !msg_bytes_max) return set_error(GOSSIP_EINVAL, "NULL argument");
+    if (e->opt_rehearse_rows < 2 || ranges != (uint32_t)e->opt_rehearse_rows)
+        return set_error(GOSSIP_EINVAL, "get_rehearsal_peak: ranges must equal the rehearse_rows option");
+    for (uint32_t r = 0; r < ranges; r++) msg_bytes_max[r] = r < e->rr_bytes_max.size() ? e->rr_bytes_max[r] : 0;
     return GOSSIP_OK;
 }
 
@@ -3784,6 +3926,7 @@ int gossip_engine_reset_timing(gossip_engine* e) {
     e->rehearse_harvest();  // (row-partition rehearsal: restart the per-range sums)
     for (auto& v : e->rr_ms) std::fill(v.begin(), v.end(), 0.0);
     std::fill(e->rr_bytes.begin(), e->rr_bytes.end(), 0ull);
+    std::fill(e->rr_bytes_max.begin(), e->rr_bytes_max.end(), 0ull);
     e->rr_ticks = 0;
     if (e->d_acct) {
         HIP_TRY(hipMemsetAsync(e->d_acct, 0, kAcctSlots * kAcctReplicas * 8, e->stream));

@@ -221,8 +221,9 @@ bool any_id_collision(uint64_t m, const gossip_gen_event* ev) {
 
 using namespace gossip;
 
-extern "C" int gossip_shard_events(const gossip_topology* t, uint64_t m, const gossip_gen_event* ev,
-                                   uint32_t shard_count, uint32_t* owner) {
+// latency_ns > 0: the birth-tick rule (gossip_shard_events_by_tick), else the hash rule
+static int shard_events_rule(const gossip_topology* t, uint64_t m, const gossip_gen_event* ev,
+                             uint32_t shard_count, int64_t latency_ns, uint32_t* owner) {
     if (!t || (m && (!ev || !owner))) return set_error(GOSSIP_EINVAL, "NULL argument");
     if (shard_count == 0) return set_error(GOSSIP_EINVAL, "shard_count must be >= 1");
     if (m >= (1ull << 32)) return set_error(GOSSIP_EINVAL, "more than 2^32 - 1 events");
@@ -243,6 +244,22 @@ extern "C" int gossip_shard_events(const gossip_topology* t, uint64_t m, const g
             }
         key = std::vector<uint64_t>();
         if (collision) topology_components(t);
+        if (latency_ns > 0) {
+            // birth-tick rule: the first generation of the instance (lone: the event itself)
+            std::unordered_map<uint64_t, int64_t> first;  // (id, component) -> earliest ns
+            if (collision)
+                for (uint64_t k = 0; k < m; k++)
+                    if (!lone[k]) {
+                        const uint64_t ik = ((uint64_t)ev[k].share_id << 32) | t->comp[ev[k].node];
+                        auto it = first.find(ik);
+                        if (it == first.end() || ev[k].ns < it->second) first[ik] = ev[k].ns;
+                    }
+            for (uint64_t k = 0; k < m; k++) {
+                const int64_t ns = lone[k] ? ev[k].ns : first[((uint64_t)ev[k].share_id << 32) | t->comp[ev[k].node]];
+                owner[k] = (uint32_t)((uint64_t)(ns / latency_ns) % shard_count);
+            }
+            return GOSSIP_OK;
+        }
         for (uint64_t k = 0; k < m; k++) {
             const uint64_t h = lone[k] ? instance_hash(ev[k].share_id, ev[k].node, true)
                                        : instance_hash(ev[k].share_id, t->comp[ev[k].node], false);
@@ -252,6 +269,17 @@ extern "C" int gossip_shard_events(const gossip_topology* t, uint64_t m, const g
     } catch (const std::bad_alloc&) {
         return set_error(GOSSIP_ENOMEM, "host allocation failed");
     }
+}
+
+extern "C" int gossip_shard_events(const gossip_topology* t, uint64_t m, const gossip_gen_event* ev,
+                                   uint32_t shard_count, uint32_t* owner) {
+    return shard_events_rule(t, m, ev, shard_count, 0, owner);
+}
+
+extern "C" int gossip_shard_events_by_tick(const gossip_topology* t, uint64_t m, const gossip_gen_event* ev,
+                                           uint32_t shard_count, int64_t latency_ns, uint32_t* owner) {
+    if (latency_ns <= 0) return set_error(GOSSIP_EINVAL, "latency_ns must be > 0");
+    return shard_events_rule(t, m, ev, shard_count, latency_ns, owner);
 }
 
 extern "C" {

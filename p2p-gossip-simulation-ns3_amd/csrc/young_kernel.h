@@ -163,7 +163,7 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
 }
 
 // Diagnostic build YOUNG_STAMPS: shader cycles per phase of the node loop (s_memtime), summed
-// over waves into acct[20..27] (engine.hip prints them with the counters); no output depends on them
+// over waves into acct[22..29] (engine.hip prints them with the counters); no output depends on them
 #ifdef YOUNG_STAMPS
 #define YSTAMP(k)                                              \
     do {                                                       \
@@ -608,7 +608,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
     }
 #ifdef YOUNG_STAMPS
     if (a.acct && lane_id == 0)
-        for (int k = 0; k < 8; k++) acct_add(a.acct, 20u + (uint32_t)k, (unsigned long long)ycyc[k]);
+        for (int k = 0; k < 8; k++) acct_add(a.acct, 22u + (uint32_t)k, (unsigned long long)ycyc[k]);
 #endif
     if (a.acct && lane_id == 0) {
         const uint32_t tv[11] = {t_sl, t_col, t_fb, t_srd, t_swr, t_rw, t_slw, t_miss, t_lr, t_lw, t_mat};

@@ -36,6 +36,7 @@ F_NOSKIP = 4
 F_TILE_PER_TICK = 32
 F_HANDSHAKE = 64
 F_HOP_BATCH = 128
+F_SHARD_BY_TICK = 256
 
 EXPORTED_SYMBOLS = (
     "gossip_last_error", "gossip_version", "gossip_seconds_to_ns", "gossip_milliseconds_to_ns",
@@ -43,7 +44,7 @@ EXPORTED_SYMBOLS = (
     "gossip_topology_num_links", "gossip_topology_get_links", "gossip_topology_num_entries",
     "gossip_topology_get_csr", "gossip_topology_get_degrees", "gossip_topology_destroy",
     "gossip_schedule_create", "gossip_schedule_from_events", "gossip_schedule_size",
-    "gossip_schedule_get", "gossip_schedule_destroy", "gossip_shard_events",
+    "gossip_schedule_get", "gossip_schedule_destroy", "gossip_shard_events", "gossip_shard_events_by_tick",
     "gossip_engine_create", "gossip_engine_set_graph", "gossip_engine_set_topology",
     "gossip_engine_set_schedule", "gossip_engine_set_schedule_obj", "gossip_engine_add_snapshot",
     "gossip_engine_first_tick", "gossip_engine_end_tick", "gossip_engine_current_tick",
@@ -58,7 +59,8 @@ EXPORTED_SYMBOLS = (
     "gossip_schedule_create_philox", "gossip_engine_exchange_chunks",
     "gossip_engine_exchange_export_chunk", "gossip_engine_exchange_import_chunk",
     "gossip_format_netanim", "gossip_topology_load_links", "gossip_schedule_load_events",
-    "gossip_engine_abort", "gossip_engine_get_rehearsal",
+    "gossip_engine_abort", "gossip_engine_get_rehearsal", "gossip_engine_get_rehearsal_peak",
+    "gossip_engine_get_option",
 )
 
 # NS-3 5 Mbps point-to-point links (p2pnetwork.cc:113): ns per byte, PPP+IPv4+TCP(timestamp
@@ -112,6 +114,8 @@ class gossip_counters(C.Structure):
         ("pull_sat_skips", C.c_uint64), ("pull_sat", C.c_uint32), ("pad0", C.c_uint32),
         ("window_early_retires", C.c_uint64), ("young_list_lines", C.c_uint64),
         ("pull_items", C.c_uint64), ("pull_gather_items", C.c_uint64),
+        ("dense_fused_launches", C.c_uint64),
+        ("young_grid", C.c_uint32), ("pad1", C.c_uint32),
     ]
 
 
@@ -142,6 +146,8 @@ def load_library(path: str = LIB_PATH):
         "gossip_schedule_load_events": (C.c_int, [u32, C.c_char_p, C.POINTER(P)]),
         "gossip_engine_abort": (C.c_int, [P]),
         "gossip_engine_get_rehearsal": (C.c_int, [P, u32, P, P, P, P, C.POINTER(u64)]),
+        "gossip_engine_get_rehearsal_peak": (C.c_int, [P, u32, P]),
+        "gossip_engine_get_option": (C.c_int, [P, C.c_char_p, C.POINTER(i64)]),
         "gossip_topology_num_nodes": (u32, [P]),
         "gossip_topology_num_links": (u64, [P]),
         "gossip_topology_get_links": (C.c_int, [P, P, P]),
@@ -156,6 +162,7 @@ def load_library(path: str = LIB_PATH):
         "gossip_schedule_get": (C.c_int, [P, P]),
         "gossip_schedule_destroy": (None, [P]),
         "gossip_shard_events": (C.c_int, [P, u64, P, u32, P]),
+        "gossip_shard_events_by_tick": (C.c_int, [P, u64, P, u32, i64, P]),
         "gossip_engine_create": (C.c_int, [C.POINTER(gossip_config), C.POINTER(P)]),
         "gossip_engine_set_graph": (C.c_int, [P, u32, P, P, P]),
         "gossip_engine_set_topology": (C.c_int, [P, P]),
@@ -358,12 +365,17 @@ def make_schedule_philox(n: int, seed: int, t_start_ns: int, t_cut_ns: int, t_ge
         lib.gossip_schedule_destroy(h)
 
 
-def shard_events(topo: "Topology", ev: np.ndarray, shard_count: int) -> np.ndarray:
-    """Owner shard of every generation event (the engines' multi-GPU sharding rule)."""
+def shard_events(topo: "Topology", ev: np.ndarray, shard_count: int, by_tick_latency_ns: int = 0) -> np.ndarray:
+    """Owner shard of every generation event (the engines' multi-GPU sharding rule): the hash rule,
+    or with by_tick_latency_ns > 0 the birth-tick rule of GOSSIP_F_SHARD_BY_TICK."""
     ev = np.ascontiguousarray(ev, GEN_EVENT_DTYPE)
     owner = np.empty(ev.size, np.uint32)
-    _check(load_library().gossip_shard_events(topo._h, ev.size, _vp(ev), shard_count, _vp(owner)),
-           "shard events")
+    lib = load_library()
+    if by_tick_latency_ns > 0:
+        rc = lib.gossip_shard_events_by_tick(topo._h, ev.size, _vp(ev), shard_count, int(by_tick_latency_ns), _vp(owner))
+    else:
+        rc = lib.gossip_shard_events(topo._h, ev.size, _vp(ev), shard_count, _vp(owner))
+    _check(rc, "shard events")
     return owner
 
 
@@ -419,10 +431,16 @@ class Engine:
                "row partition")
 
     def set_option(self, name: str, value: int):
-        """Tuning option (gossip.h gossip_engine_set_option): pull_nt, pull_grid, pull_lpw,
-        dense_min_tiles.  Results never depend on them."""
+        """Tuning option (gossip.h gossip_engine_set_option): pull_nt, pull_grid, young, ...,
+        dense_fused.  Results never depend on them."""
         _check(load_library().gossip_engine_set_option(self._h, name.encode(), int(value)),
                f"option {name}")
+
+    def get_option(self, name: str) -> int:
+        """The value option `name` holds (gossip_engine_get_option)."""
+        v = C.c_int64()
+        _check(load_library().gossip_engine_get_option(self._h, name.encode(), C.byref(v)), f"option {name}")
+        return int(v.value)
 
     def connect_rccl(self, unique_id: bytes):
         _check(load_library().gossip_engine_connect_rccl(self._h, unique_id, len(unique_id)),
@@ -539,13 +557,17 @@ class Engine:
 
     def rehearsal(self, ranges: int) -> dict:
         """Option rehearse_rows = ranges: per row block, summed since reset_timing -- pull, pack
-        and unpack time (ms) and message bytes, and the number of ticks rehearsed."""
+        and unpack time (ms) and message bytes, the number of ticks rehearsed, and the largest
+        message of one tick (msg_bytes_max)."""
         pull, pack, unpack = (np.zeros(ranges) for _ in range(3))
         msg = np.zeros(ranges, np.uint64)
         ticks = C.c_uint64()
         _check(load_library().gossip_engine_get_rehearsal(self._h, ranges, _vp(pull), _vp(pack), _vp(unpack),
                                                           _vp(msg), C.byref(ticks)), "rehearsal")
-        return dict(pull_ms=pull, pack_ms=pack, unpack_ms=unpack, msg_bytes=msg, ticks=int(ticks.value))
+        peak = np.zeros(ranges, np.uint64)
+        _check(load_library().gossip_engine_get_rehearsal_peak(self._h, ranges, _vp(peak)), "rehearsal peak")
+        return dict(pull_ms=pull, pack_ms=pack, unpack_ms=unpack, msg_bytes=msg, ticks=int(ticks.value),
+                    msg_bytes_max=peak)
 
     def trace(self):
         lib = load_library()

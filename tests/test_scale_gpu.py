@@ -311,8 +311,11 @@ def test_c5_mfma_equals_csr_and_oracle_b(gossip, oracle, c5):
     n = topo.num_nodes
     t_cut = W.T0_NS + 40 * W.L_NS
     dense, cd = _run(gossip, topo, ev, W.T0_NS, t_cut, mode=gossip.MODE_DENSE)
+    assert cd.dense_fused_launches == cd.pull_launches
     csr, _ = _run(gossip, topo, ev, W.T0_NS, t_cut, mode=gossip.MODE_CSR)
     _same(dense, csr, what="C5 MFMA vs CSR, 4096 shares")
+    three, _ = _run(gossip, topo, ev, W.T0_NS, t_cut, mode=gossip.MODE_DENSE, options=(("dense_fused", 0),))
+    _same(dense, three, what="C5 fused vs three-kernel MFMA, 4096 shares")
     _invariants(dense, cd)
     assert cd.dense_ops > 0 and int(dense.recv.sum()) == len(ev) * (n - 1)  # diameter 2: all reached
     sub = ev[:64]
@@ -358,6 +361,8 @@ def test_c2_full_run_all_paths_match_oracle_b(gossip, oracle):
     assert ref.edge_events > 1e11
     runs = [("MFMA tick-by-tick", dict(mode=gossip.MODE_DENSE)),
             ("MFMA hop-batched", dict(mode=gossip.MODE_DENSE, flags=gossip.F_HOP_BATCH)),
+            ("MFMA hop-batched, three kernels", dict(mode=gossip.MODE_DENSE, flags=gossip.F_HOP_BATCH,
+                                                     options=(("dense_fused", 0),))),
             ("CSR hop-batched", dict(mode=gossip.MODE_CSR, flags=gossip.F_HOP_BATCH)),
             ("AUTO", dict())]
     for name, kw in runs:
@@ -366,6 +371,8 @@ def test_c2_full_run_all_paths_match_oracle_b(gossip, oracle):
         assert c.edge_events == ref.edge_events
         if name == "AUTO":
             assert c.dense_ops > 0  # AUTO picks the MFMA path on a p = 0.3 graph
+        if name.startswith("MFMA"):  # every MFMA tick fused (unique ids) unless switched off
+            assert c.dense_fused_launches == (0 if "three" in name else c.pull_launches), name
 
 
 def test_c2_golden_fixture_on_every_path(gossip):

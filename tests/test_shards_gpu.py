@@ -48,13 +48,46 @@ T0 = 5_000_000_000
 
 
 def _burst(gossip):
-    """4,096 distinct shares born in one tick of a 20,000-node sparse graph: a 96-word window
-    (48.5 MB of bitmaps, graph, counters, occupancy and saturation words) for one engine, 80 words
-    (40.8 MB) for each of 2 shards -- so a 44 MB budget takes exactly 2 (tools/diag/shard_fallback.py)."""
+    """4,096 distinct shares born in one tick of a 20,000-node sparse graph: one engine's window
+    must hold all of them, each of 2 shards about half (tools/diag/shard_fallback.py)."""
     rng = np.random.Generator(np.random.Philox(11))
     nodes = rng.choice(N_BURST, size=4096, replace=False)
     return gossip.events_from_arrays(T0 + 1000 + np.arange(4096, dtype=np.int64), nodes,
                                      np.arange(1, 4097, dtype=np.uint32))
+
+
+def _budget(gossip, ev):
+    """A device-memory budget between what 2 shards and what 1 engine hold for the burst, from the
+    engines' own reported need (gossip_counters.device_bytes after an unconstrained run) -- not a
+    constant, so the test follows any change of the engine's layout."""
+    topo = gossip.Topology.gnp(N_BURST, 16.0 / (N_BURST - 1), 8, gossip.TOPO_SKIP)
+    t_cut = gossip.seconds_to_ns(5.2)
+
+    def run(shards, r, max_words=0):
+        eng = gossip.Engine(N_BURST, 5_000_000, T0, t_cut, shard_rank=r, shard_count=shards, max_words=max_words)
+        eng.set_topology(topo)
+        eng.set_schedule(ev)
+        eng.run()
+        eng.sync()
+        c = eng.counters()
+        eng.close()
+        return c
+
+    def need(shards):
+        # the window the run reached (an unconstrained engine also allocates headroom), then the
+        # bytes an engine holds with exactly that window
+        out = 0
+        for r in range(shards):
+            hw = run(shards, r).words_hw
+            c = run(shards, r, max_words=hw)
+            out = max(out, c.device_bytes)
+        return out
+
+    one, two = need(1), need(2)
+    assert two < one, (one, two)
+    mib = (one + two) // 2 >> 20  # (the CLI takes whole MB)
+    assert two < mib << 20 < one, (one, two, mib)
+    return mib
 
 
 def test_cli_falls_back_to_more_shards(gossip, tmp_path):
@@ -64,7 +97,7 @@ def test_cli_falls_back_to_more_shards(gossip, tmp_path):
     base = [f"--numNodes={N_BURST}", f"--connectionProb={16.0 / (N_BURST - 1)}", "--simTime=5.3",
             "--seed=8", f"--events={evf}", "--quiet"]
     one = _sim(*base)
-    lim = _sim(*base, "--memLimitMB=44")
+    lim = _sim(*base, f"--memLimitMB={_budget(gossip, ev)}")
     assert "retrying with 2" in lim.stderr
     assert "engines: 2 share shards" in lim.stdout
     assert _report(lim.stdout) == _report(one.stdout)
@@ -72,7 +105,7 @@ def test_cli_falls_back_to_more_shards(gossip, tmp_path):
 
 def test_simulation_falls_back_to_more_shards(gossip, oracle):
     ev = _burst(gossip)
-    sim = gossip.P2PGossipNetworkSimulation(N_BURST, topo_seed=8, options={"mem_limit": 44 << 20})
+    sim = gossip.P2PGossipNetworkSimulation(N_BURST, topo_seed=8, options={"mem_limit": _budget(gossip, ev) << 20})
     sim.CreateRandomTopology(16.0 / (N_BURST - 1), 5.0)
     st = sim.Start(5.3, events=ev)
     assert sim.shards_used == 2

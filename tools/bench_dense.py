@@ -4,8 +4,8 @@ bit-sliced CSR pull (GOSSIP_MODE_CSR) on the same dense workload.  One JSON line
 
     python tools/bench_dense.py c2            # C2: 4,096 nodes, p=0.3, full 60 s, real time
     python tools/bench_dense.py c2 --batch    # the same run hop-batched (GOSSIP_F_HOP_BATCH)
-    python tools/bench_dense.py c5 --width 512 # C5 slice: 65,536 nodes, p=0.3, one flood batch
-                                               # of `width` concurrent shares, 1 GPU
+    python tools/bench_dense.py c5             # C5 slice: 65,536 nodes, p=0.3, one flood batch
+                                               # of --width concurrent shares (default: C5's 4,096), 1 GPU
 
 MFMA utilisation = 2*M*N*K of the computed 128x128 output tiles / time / 5 POPS (the dense int8
 peak: 2x the 2.5 PF dense bf16 rate, MI355X_MICROARCH.md "Matrix cores"), over the MFMA kernel
@@ -46,7 +46,7 @@ def run(topo, ev, t_cut, mode, tick_end=None, flags=0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("config", choices=["c2", "c5"])
-    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--width", type=int, default=4096, help="C5 shares in the flood batch (BASELINE C5: 4,096)")
     ap.add_argument("--nodes", type=int, default=0)
     ap.add_argument("--modes", default="csr,dense")
     ap.add_argument("--batch", action="store_true", help="hop-batched run (GOSSIP_F_HOP_BATCH)")
