@@ -58,12 +58,14 @@ constexpr uint32_t kDensePad = kStageK;            // n_pad multiple (tile and s
 static_assert(kStageK % 512u == 0u && ((kStageRow / 16u) & 1u), "stage: odd 16-B row pitch");
 
 // Frontier bitmap (node rows of share words) -> one bit row per share column.  A wave takes
-// 64 nodes x one word and transposes the 64 x 64 bit block with ballots.
+// 64 nodes x one word and transposes the 64 x 64 bit block with ballots.  snz (nullable): the
+// fused kernel's stage masks, bit (chunk / 16) of column tile w / 4 set where the block is non-zero.
 __global__ __launch_bounds__(256) void k_transpose(const uint64_t* __restrict__ F, uint32_t stride,
                                                    uint32_t n, uint32_t kw, uint32_t nwords,
                                                    const unsigned long long* live_prev,
                                                    const unsigned long long* __restrict__ nz,
-                                                   uint32_t ntw, uint32_t* __restrict__ FT) {
+                                                   uint32_t ntw, uint32_t* __restrict__ FT,
+                                                   unsigned long long* snz, uint32_t nstw) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t chunk = blockIdx.x * 4u + wave_in_block();  // 64-node chunk
     const uint32_t w = blockIdx.y;
@@ -85,6 +87,10 @@ __global__ __launch_bounds__(256) void k_transpose(const uint64_t* __restrict__ 
     // row c = 64w + lane; this chunk's 64 node bits are words 2*chunk, 2*chunk+1 of the row
     uint64_t* row = reinterpret_cast<uint64_t*>(FT + (uint64_t)(w * 64u + lane) * kw);
     row[chunk] = keep;
+    if (snz && __ballot(keep != 0ull) && lane == 0) {
+        const uint32_t st = chunk / 16u;  // 1,024-node K stage
+        atomicOr(&snz[(uint64_t)(w >> 2) * nstw + (st >> 6)], 1ull << (st & 63u));
+    }
 }
 
 __device__ __forceinline__ v4i_t dense_expand(uint32_t x, const uint32_t (&m)[4]) {
@@ -360,11 +366,21 @@ __global__ __launch_bounds__(1024) void k_dense_dedup(PullArgs a) {
 // dependent launch cost ~6 us of dispatch gap and k_dense_bits itself paid a prologue, a 3-barrier
 // zero-stage test per stage and an epilogue per 256 x 256 tile with nothing to overlap them.
 //
-// Work: one block per CU walks its tiles (256 rows x 256 columns) in an XCD-major order (the
-// column tiles of one row block run on one XCD together, the adjacency rows stay in its L2).
-// Per tile only the K stages whose frontier bits are non-zero are computed: the producer of FT
-// (this kernel's epilogue at t-1, plus k_births) sets a per-(column tile, stage) bit, so an empty
-// stage is neither loaded nor multiplied.  Stages arrive by LDS-DMA (global_load_lds_dwordx4,
+// Work: tiles of 256 rows x 256 columns; per tile only the K stages whose frontier bits are
+// non-zero are computed: the producer of FT (this kernel's epilogue at t-1, plus k_births, or
+// k_transpose) sets a per-(column tile, stage) bit, so an empty stage is neither loaded nor
+// multiplied.  A (tile, non-empty stage) pair is a UNIT.  Schedule: one block per CU; the live
+// tiles (tile order, row block major) go out in data-parallel ROUNDS, block b taking tile r G + b
+// in round r (the blocks of one XCD take adjacent tiles: the column tiles of one row block, whose
+// adjacency rows then stay in that XCD's L2), and the last partial round -- the tail, fewer tiles
+// than blocks -- is split stream-K: its units are cut into G equal contiguous ranges, so no CU
+// waits for a whole tile while others idle (C2: ~600 live tiles of 4 stages on 256 CUs).  A tile
+// split between blocks is reduced by OR: Inc > 0 iff some partial sum is > 0 (all products are
+// >= 0), so each block ORs its partial row words into `inc` (atomics), counts its units into the
+// tile's ticket, and the block that completes the ticket takes the words back (atomic exchange
+// with 0) and runs the epilogue.  (Pure stream-K over all units -- one contiguous range per block
+// -- measured slower on C5: each block then streams adjacency rows no other block of its XCD is
+// reading, 11.0 / 9.98 ms per full tick against 9.36 / 8.99 ms in rounds.)  Stages arrive by LDS-DMA (global_load_lds_dwordx4,
 // 16 B per lane, no VGPR staging) into two 64-KB buffers; the next (tile, stage) is issued as soon
 // as the current one has landed -- across tile boundaries, so the next tile's first stage loads
 // while this tile's epilogue runs.  The LDS image is lane-linear per 1-KiB DMA piece (8 rows of
@@ -372,8 +388,14 @@ __global__ __launch_bounds__(1024) void k_dense_dedup(PullArgs a) {
 // p ^ ((r >> 1) & 7) -- so the 16 lanes of a ds_read_b128 (16 consecutive rows, one chunk) hit 16
 // distinct 16-B bank groups.
 //
-// Epilogue per tile (every column tile of the window, dead ones included, so F_next and FT_next
-// are written whole and need no occupancy test): Inc > 0 -> row words (wave ballots) -> LDS;
+// Active tiles.  A 16-word tile of the window is ACTIVE this tick if some word of it was live last
+// tick, is (re)allocated (WF_CLEAR) or takes a generation (WF_BIRTH).  The 4 column tiles of an
+// active tile run the epilogue below even when they compute nothing, so F_next and FT_next are
+// written whole there (zeros included) and need no occupancy test; occupancy bit = active.  An
+// inactive tile is skipped: its F_next rows keep stale words behind a clear occupancy bit (k_births
+// writes a fresh row whole), and its stale FT rows are never read (no word of it can be live next
+// tick: nothing arrives in it and no generation lands in it).
+// Epilogue per tile: Inc > 0 -> row words (wave ballots) -> LDS;
 // per (row, word pair) new = inc & ~seen & keep, seen |= new, F_next = new, recv += popcount;
 // then each wave transposes two 64 x 64 bit blocks of `new` (6 shuffle-and-mask steps) into the
 // FT_next rows of its 64 columns, whose non-zero lanes give the word's liveness by ballot.
@@ -403,15 +425,27 @@ struct FusedArgs {
     uint32_t nst, nstw;                    // K stages, stage-mask words per column tile
     uint32_t mb, nt, total;                // row blocks, column tiles, mb * nt
     uint32_t wact;                         // window words: occupancy bits of tiles < wact / 16
+    unsigned long long* inc;               // n x stride words: partial Inc > 0 of split tiles (zero between uses)
+    uint32_t* tix;                         // per tile: units reduced so far (zero between uses)
+    uint32_t rmax;                         // most data-parallel rounds (A/B: GOSSIP_DENSE_ROUNDS)
+    uint32_t gm;                           // row blocks per tile group (tile order, header comment)
 };
 
 constexpr uint32_t kFStageBytes = 2u * kDenseTile * 128u;  // A + B rows of one 1024-k stage
 constexpr uint32_t kFIncOff = 2u * kFStageBytes;           // 256 rows x 4 words of inc / new
 constexpr uint32_t kFMiscOff = kFIncOff + kDenseTile * 4u * 8u;
-constexpr uint32_t kFLdsBytes = kFMiscOff + 64u;
+constexpr uint32_t kFActWords = 8;                          // active-tile bits: windows <= 8,192 words
+constexpr uint32_t kFActOff = kFMiscOff + 64u;
+constexpr uint32_t kFMaxCt = kFActWords * 64u * 4u;         // column tiles of the widest window
+constexpr uint32_t kFCtOff = kFActOff + kFActWords * 8u;    // per column tile: units, prefix (u32)
+constexpr uint32_t kFLctOff = kFCtOff + 2u * kFMaxCt * 4u;  // the column tiles with units, in order (u16)
+constexpr uint32_t kFLdsBytes = kFLctOff + kFMaxCt * 2u;
+static_assert(kFLdsBytes <= 163840u, "k_dense_fused LDS");
 static_assert(kStageK == 1024u, "k_dense_fused stages 128-B rows");
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
+
+
 
 // One LDS-DMA piece: 16 B per lane from gsrc to LDS byte address lds_dst + 16 x lane.  Inline asm,
 // not __builtin_amdgcn_global_load_lds: for the builtin hipcc cannot tell which LDS bytes the DMA
@@ -463,49 +497,230 @@ __device__ __forceinline__ bool fused_tile_live(const FusedArgs& a, uint32_t w0)
     return (a.live_prev[w0] | a.live_prev[w0 + 1] | a.live_prev[w0 + 2] | a.live_prev[w0 + 3]) != 0ull;
 }
 
-// 64 x 64 bit transpose across a wave: lane r holds row r (bit c = column c) on entry, column r
-// (bit r' = row r') on exit
-__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x, uint32_t lane) {
-#pragma unroll
-    for (int j = 32; j >= 1; j >>= 1) {
-        const uint64_t lo = j == 32 ? 0x00000000ffffffffull
-                          : j == 16 ? 0x0000ffff0000ffffull
-                          : j == 8 ? 0x00ff00ff00ff00ffull
-                          : j == 4 ? 0x0f0f0f0f0f0f0f0full
-                          : j == 2 ? 0x3333333333333333ull
-                                   : 0x5555555555555555ull;
-        const uint64_t y = __shfl_xor(x, j, 64);
-        x = (lane & (uint32_t)j) ? ((x & ~lo) | ((y >> j) & lo)) : ((x & lo) | ((y & lo) << j));
+// x of lane (lane ^ J), every lane active: DPP quad permutes (J = 1, 2), row shifts both ways
+// (J = 4, 8) and gfx950's permlane swaps (J = 16, 32) -- VALU only, no ds_bpermute round trip
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t x, uint32_t lane) {
+    if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);
+    if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);
+    if constexpr (J == 4 || J == 8) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + J, 0xF, 0xF, false);  // row_shl: lane + J
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x110 + J, 0xF, 0xF, false);  // row_shr: lane - J
+        return (lane & (uint32_t)J) ? dn : up;
+    }
+    if constexpr (J == 16) {  // swaps the odd 16-lane rows of the first operand with the even rows of the second
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (lane & 16u) ? (uint32_t)r[0] : (uint32_t)r[1];
+    }
+    if constexpr (J == 32) {  // swaps the upper 32 lanes of the first operand with the lower 32 of the second
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (lane & 32u) ? (uint32_t)r[0] : (uint32_t)r[1];
     }
     return x;
 }
 
+template <int J>
+__device__ __forceinline__ uint64_t transpose_step(uint64_t x, uint32_t lane, uint64_t lo) {
+    const uint64_t y = ((uint64_t)lane_xor<J>((uint32_t)(x >> 32), lane) << 32) | lane_xor<J>((uint32_t)x, lane);
+    return (lane & (uint32_t)J) ? ((x & ~lo) | ((y >> J) & lo)) : ((x & lo) | ((y & lo) << J));
+}
+
+// 64 x 64 bit transpose across a wave: lane r holds row r (bit c = column c) on entry, column r
+// (bit r' = row r') on exit (block swaps of 32, 16, ..., 1)
+__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x, uint32_t lane) {
+    x = transpose_step<32>(x, lane, 0x00000000ffffffffull);
+    x = transpose_step<16>(x, lane, 0x0000ffff0000ffffull);
+    x = transpose_step<8>(x, lane, 0x00ff00ff00ff00ffull);
+    x = transpose_step<4>(x, lane, 0x0f0f0f0f0f0f0f0full);
+    x = transpose_step<2>(x, lane, 0x3333333333333333ull);
+    x = transpose_step<1>(x, lane, 0x5555555555555555ull);
+    return x;
+}
+
+// Diagnostic build DENSE_STAMPS: shader cycles per phase of k_dense_fused (s_memtime), summed over
+// waves into acct[22..29] (engine.hip prints them); no output depends on them.  0 prologue, 1 stage
+// wait + barrier, 2 stage issue + MFMA, 3 ballots, 4 split-tile reduction, 5 epilogue dedup,
+// 6 epilogue transpose + liveness, 7 epilogue-only tiles
+#ifdef DENSE_STAMPS
+#define DSTAMP(k)                                              \
+    do {                                                       \
+        const uint64_t ds_t = __builtin_amdgcn_s_memtime();    \
+        dcyc[k] += ds_t - dlast;                               \
+        dlast = ds_t;                                          \
+    } while (0)
+#else
+#define DSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+
 __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
+#ifdef DENSE_STAMPS
+    uint64_t dcyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t dlast = __builtin_amdgcn_s_memtime();
+    const uint64_t drt0 = __builtin_amdgcn_s_memrealtime(), dmt0 = dlast;  // (block time, 100 MHz; clock calibration)
+#endif
     __shared__ __attribute__((aligned(16))) uint8_t S[kFLdsBytes];
     unsigned long long* sInc = reinterpret_cast<unsigned long long*>(S + kFIncOff);
-    unsigned long long* sMisc = reinterpret_cast<unsigned long long*>(S + kFMiscOff);  // [0..3] live, [4] any
+    unsigned long long* sMisc = reinterpret_cast<unsigned long long*>(S + kFMiscOff);  // [0..3] live, [4] any, [5] flag, [6] wave sums
+    unsigned long long* sAct = reinterpret_cast<unsigned long long*>(S + kFActOff);
+    uint32_t* sCtU = reinterpret_cast<uint32_t*>(S + kFCtOff);  // units of column tile ct (any row block)
+    uint32_t* sCtP = sCtU + kFMaxCt;                             // exclusive prefix of sCtU
+    uint16_t* sLct = reinterpret_cast<uint16_t*>(S + kFLctOff);  // column tiles with units, in order
     const uint32_t t = threadIdx.x, lane = t & 63u, wid = wave_in_block();
     const uint32_t wm = wid >> 2, wn = wid & 3u;
-    // XCD-major walk: block b runs on XCD b % 8 (speed only); XCD x owns tiles [x per, (x+1) per)
-    const uint32_t nx = gridDim.x >= 8u ? 8u : 1u;
-    const uint32_t xcd = blockIdx.x % nx, bpx = gridDim.x / nx, bi = blockIdx.x / nx;
-    const uint32_t per = (a.total + nx - 1u) / nx;
-    const uint32_t tlo = xcd * per, thi = min(a.total, tlo + per);
-    for (uint32_t i = blockIdx.x * 512u + threadIdx.x; i < a.snz_zwords; i += gridDim.x * 512u) a.snz_z[i] = 0ull;
-    if (bi >= bpx) return;  // (gridDim.x is a multiple of 8 when >= 8)
+    for (uint32_t i = blockIdx.x * 512u + t; i < a.snz_zwords; i += gridDim.x * 512u) a.snz_z[i] = 0ull;
+    // Per column tile ct (thread t, +512): its 4 flag bytes, its 4 live_prev words and its stage
+    // masks, all loaded before any is used (one round trip).  Active 16-word tiles (header comment:
+    // 4 column tiles, lanes 4k..4k+3) -> LDS bitmap, then F_next's occupancy words; units per column
+    // tile: its non-empty stages if its tile is active and the column tile was live last tick.
+    if (t < kFActWords) sAct[t] = 0ull;
+    __syncthreads();
+    for (uint32_t ct0 = 0; ct0 < a.nt; ct0 += 512u) {  // (uniform trip count: the quad shuffles see every lane)
+        const uint32_t ct = ct0 + t;
+        const bool in = ct < a.nt;
+        uint32_t f = 0u, u = 0u;
+        uint64_t lp = 0ull;
+        if (in) {
+            f = *reinterpret_cast<const uint32_t*>(a.wflags + ct * 4u);
+            if (a.live_prev) {
+                const ulonglong2* p = reinterpret_cast<const ulonglong2*>(a.live_prev + ct * 4u);
+                const ulonglong2 x = p[0], y = p[1];
+                lp = x.x | x.y | y.x | y.y;
+            } else {
+                lp = ~0ull;
+            }
+            for (uint32_t s0 = 0; s0 < a.nst; s0 += 64u) u += (uint32_t)__popcll(fused_stages(a, ct, s0));
+        }
+        uint32_t c = (in && (lp != 0ull || (f & (0x01010101u * (WF_CLEAR | WF_BIRTH))) != 0u)) ? 1u : 0u;
+        c |= lane_xor<1>(c, lane);
+        c |= lane_xor<2>(c, lane);
+        if (in) {
+            if ((ct & 3u) == 0u && c) atomicOr(&sAct[ct >> 8], 1ull << ((ct >> 2) & 63u));
+            sCtU[ct] = (c && lp != 0ull) ? u : 0u;
+        }
+    }
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * 512u + t; i < (uint64_t)a.n * a.ntw; i += (uint64_t)gridDim.x * 512u)
+        a.nz_next[i] = sAct[i % a.ntw];
+    auto active = [&](uint32_t ct) -> bool { return (sAct[ct >> 8] >> ((ct >> 2) & 63u)) & 1ull; };
+    // exclusive prefix over the column tiles of (units << 12 | live), so the same scan places the
+    // live column tiles: each thread sums a run of them, the block scans the runs (units < 2^20:
+    // nt <= 2,048 column tiles x <= 512 stages)
+    const uint32_t run = (a.nt + 511u) / 512u, c0 = t * run;
+    uint32_t mine = 0;
+    for (uint32_t c = c0; c < min(a.nt, c0 + run); c++) mine += (sCtU[c] << 12) | (sCtU[c] ? 1u : 0u);
+    uint32_t incl = mine;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, off, 64);
+        if (lane >= (uint32_t)off) incl += y;
+    }
+    uint32_t* sWave = reinterpret_cast<uint32_t*>(sInc);  // 8 wave totals (sInc is free until the first tile)
+    if (lane == 63u) sWave[wid] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, rowU = 0;
+    for (uint32_t q = 0; q < 8u; q++) {
+        const uint32_t x = sWave[q];
+        if (q < wid) wbase += x;
+        rowU += x;
+    }
+    {
+        uint32_t p = wbase + incl - mine;
+        for (uint32_t c = c0; c < min(a.nt, c0 + run); c++) {
+            sCtP[c] = p >> 12;
+            if (sCtU[c]) sLct[p & 4095u] = (uint16_t)c;
+            p += (sCtU[c] << 12) | (sCtU[c] ? 1u : 0u);
+        }
+    }
+    __syncthreads();
+    const uint32_t nlc = rowU & 4095u;  // (packed: units in the high bits, live column tiles in the low 12)
+    rowU >>= 12;
+    // blocks in XCD-major order (block b runs on XCD b % 8: adjacent ords share an XCD)
+    const uint32_t G = gridDim.x;
+    const uint32_t nx = G >= 8u ? 8u : 1u;
+    const uint32_t ord = (blockIdx.x % nx) * (G / nx) + blockIdx.x / nx;
+    // Tile order: groups of GM row blocks; within a group, column tile major, then row block; each
+    // tile's units (its non-empty stages) contiguous.  32 consecutive tiles -- the blocks of one XCD
+    // in a round -- then span GM row blocks x 32 / GM column tiles: per stage they read GM
+    // adjacency tiles and 32 / GM FT tiles through that XCD's L2, not 1 + 32 (row-major order)
+    const uint32_t GM = a.gm;
+    const uint64_t GU = (uint64_t)GM * rowU;   // units of a full group
+    const uint64_t U = (uint64_t)a.mb * rowU;  // units of the tick
+    const uint32_t L = a.mb * nlc;             // live tiles
+    auto grows = [&](uint32_t g) -> uint32_t { return min(GM, a.mb - g * GM); };
+    // the i-th live tile in tile order -> (row block, column tile), and its first unit
+    auto tile_at = [&](uint32_t i, uint32_t& mblk, uint32_t& ct) -> uint64_t {
+        const uint32_t g = i / (GM * nlc), j = i - g * (GM * nlc), rows = grows(g);
+        ct = sLct[j / rows];
+        const uint32_t r = j % rows;
+        mblk = g * GM + r;
+        return g * GU + (uint64_t)rows * sCtP[ct] + (uint64_t)r * sCtU[ct];
+    };
+    const uint32_t R = min(L / G, a.rmax);    // whole data-parallel rounds
+    // the tail: live tiles [R G, L), whose units fill the blocks' deficits below the mean load
+    // ceil(U / G) in ord order (column tiles differ in non-empty stages, so the rounds leave the
+    // blocks unequal; an even split of the tail would keep that difference)
+    uint64_t tail0 = U;
+    if (R * G < L) {
+        uint32_t m_, c_;
+        tail0 = tile_at(R * G, m_, c_);
+    }
+    uint64_t tu0, tu1;
+    {
+        const uint64_t Tm = (U + G - 1u) / G, Ut = U - tail0;
+        uint32_t* sTw = reinterpret_cast<uint32_t*>(sInc) + 32;  // wave totals, then the deficits'
+        uint32_t* sD = sTw + 8;                                  // prefix sD[0..G] (sInc is free here)
+        uint32_t d = 0;
+        if (t < G) {
+            uint64_t w = 0;
+            for (uint32_t k = 0; k < R; k++) {
+                uint32_t m_, c_;
+                tile_at(k * G + t, m_, c_);
+                w += sCtU[c_];
+            }
+            d = w < Tm ? (uint32_t)(Tm - w) : 0u;  // (sum of deficits <= G Tm < 2^31)
+        }
+        uint32_t di = d;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)di, off, 64);
+            if (lane >= (uint32_t)off) di += y;
+        }
+        if (lane == 63u) sTw[wid] = di;
+        __syncthreads();
+        uint32_t db = 0;
+        for (uint32_t q = 0; q < wid; q++) db += sTw[q];
+        if (t < G) sD[t + 1u] = db + di;
+        if (t == 0) sD[0] = 0u;
+        __syncthreads();
+        tu0 = tail0 + min<uint64_t>(sD[ord], Ut);
+        tu1 = tail0 + min<uint64_t>(sD[ord + 1u], Ut);
+    }
+    // this block's range k: round k's tile (k < R), then (k == R) its share of the tail
+    auto range_of = [&](uint32_t k, uint64_t& b, uint64_t& e) -> bool {
+        if (k < R) {
+            uint32_t m_, ct;
+            b = tile_at(k * G + ord, m_, ct);
+            e = b + sCtU[ct];
+            return true;
+        }
+        b = tu0;
+        e = tu1;
+        return k == R && tu0 < tu1;
+    };
 
     const uint32_t h = lane >> 5, rr = lane & 31u, sw = (rr >> 1) & 7u;
     uint32_t msk[4];
 #pragma unroll
     for (int e = 0; e < 4; e++) msk[e] = 0x01010101u << (4u * h + (uint32_t)e);
+    unsigned long long macs = 0;
+    uint32_t t_srd = 0, t_swr = 0, t_fwr = 0;
+    unsigned long long snap_local = 0;
+    const uint32_t er = t >> 1, ep = t & 1u;  // epilogue: row er, word pair ep of the tile
 
-    // the (tile, stage) sequence of this block: tiles tlo + bi, + bpx, ... ; stages by mask
-    auto tile_mb = [&](uint32_t T) { return T / a.nt; };
-    auto tile_ct = [&](uint32_t T) { return T % a.nt; };
-    // first stage >= from of tile T (a.nst if none; dead tiles have none)
-    auto first_stage = [&](uint32_t T, uint32_t from) -> uint32_t {
-        const uint32_t ct = tile_ct(T);
-        if (!fused_tile_live(a, ct * 4u)) return a.nst;
+    // the s-th non-empty stage of column tile ct, from stage `from` on (the first one: n = 0)
+    auto stage_from = [&](uint32_t ct, uint32_t from) -> uint32_t {
         while (from < a.nst) {
             const uint64_t m = fused_stages(a, ct, from);
             if (m) return from + (uint32_t)__builtin_ctzll(m);
@@ -513,49 +728,212 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
         }
         return a.nst;
     };
-    // the next (tile, stage) to load after (T, s): T == thi when none
-    uint32_t LT = tlo + bi, LS = a.nst;
-    while (LT < thi && (LS = first_stage(LT, 0u)) >= a.nst) LT += bpx;
+    // unit u -> (row block, column tile, stage); also the tile's first unit
+    auto locate = [&](uint64_t u, uint32_t& mblk, uint32_t& ct, uint32_t& st, uint64_t& tfirst) {
+        const uint32_t g = (uint32_t)(u / GU), rows = grows(g);
+        const uint32_t rem = (uint32_t)(u - g * GU);  // (< GM rowU < 2^26)
+        uint32_t lo = 0, hi = a.nt;  // last ct with rows sCtP[ct] <= rem and sCtU[ct] > 0
+        while (hi - lo > 1u) {
+            const uint32_t mid = (lo + hi) / 2u;
+            if (rows * sCtP[mid] <= rem) lo = mid; else hi = mid;
+        }
+        while (lo + 1u < a.nt && (sCtU[lo] == 0u || rows * (sCtP[lo] + sCtU[lo]) <= rem)) lo++;  // (never taken)
+        ct = lo;
+        const uint32_t rem2 = rem - rows * sCtP[ct], r = rem2 / sCtU[ct];
+        uint32_t k = rem2 - r * sCtU[ct];
+        mblk = g * GM + r;
+        tfirst = u - k;
+        st = stage_from(ct, 0u);
+        while (k--) st = stage_from(ct, st + 1u);
+    };
+
+    // ---- the epilogue's per-thread inputs (row er, words wa, wa + 1 of tile (mblk, ct)), loaded
+    //      with no dependence between them -- one round trip, issued with the tile's last stage ----
+    struct EpiIn {
+        uint32_t fa, fb;
+        uint64_t lpa, lpb;
+        ulonglong2 s2;
+    };
+    auto epi_load = [&](uint32_t mblk, uint32_t ct) -> EpiIn {
+        EpiIn e;
+        const uint32_t wa = ct * 4u + 2u * ep;
+        const uint64_t ev = (uint64_t)mblk * kDenseTile + er;
+        e.fa = a.wflags[wa];
+        e.fb = a.wflags[wa + 1];
+        e.lpa = a.live_prev ? a.live_prev[wa] : ~0ull;
+        e.lpb = a.live_prev ? a.live_prev[wa + 1] : ~0ull;
+        e.s2 = ev < a.n ? *reinterpret_cast<const ulonglong2*>(a.seen + ev * a.stride + wa) : make_ulonglong2(0ull, 0ull);
+        return e;
+    };
+    // ---- the epilogue of tile (mblk, ct): sInc holds its Inc > 0 words ----
+    auto epilogue = [&](uint32_t mblk, uint32_t ct, const EpiIn& in) {
+        const uint32_t w0 = ct * 4u;
+        const uint64_t ev = (uint64_t)mblk * kDenseTile + er;
+        const uint32_t wa = w0 + 2u * ep;
+        const uint32_t fa = in.fa, fb = in.fb;
+        const bool need_seen = ev < a.n && (((in.lpa | in.lpb) != 0ull) || ((fa | fb) & WF_CLEAR));
+        ulonglong2 s2 = in.s2;
+        DSTAMP(3);
+        uint64_t n0 = 0ull, n1 = 0ull;
+        if (ev < a.n) {
+            const uint64_t x0 = sInc[er * 4u + 2u * ep], x1 = sInc[er * 4u + 2u * ep + 1u];
+            if (fa & WF_CLEAR) s2.x = 0ull;
+            if (fb & WF_CLEAR) s2.y = 0ull;
+            const uint64_t k0 = (fa & WF_KEEP) ? a.ctl[wa].keep : ~0ull;  // (cut words only: rare)
+            const uint64_t k1 = (fb & WF_KEEP) ? a.ctl[wa + 1].keep : ~0ull;
+            n0 = x0 & ~s2.x & k0;
+            n1 = x1 & ~s2.y & k1;
+            const bool swr = (n0 | n1) != 0ull || ((fa | fb) & WF_CLEAR) != 0u;
+            if (swr) *reinterpret_cast<ulonglong2*>(a.seen + ev * a.stride + wa) = make_ulonglong2(s2.x | n0, s2.y | n1);
+            *reinterpret_cast<ulonglong2*>(a.Fnext + ev * a.stride + wa) = make_ulonglong2(n0, n1);
+            t_srd += need_seen;
+            t_swr += swr;
+            t_fwr += 1u;
+            if (a.snap) {
+                if (fa & WF_SNAP) snap_local += (unsigned long long)__popcll(n0 & a.ctl[wa].snap);
+                if (fb & WF_SNAP) snap_local += (unsigned long long)__popcll(n1 & a.ctl[wa + 1].snap);
+            }
+        }
+        uint32_t cnt = (uint32_t)(__popcll(n0) + __popcll(n1));
+        cnt += (uint32_t)__shfl_xor((int)cnt, 1, 64);
+        if (ep == 0u && cnt) atomicAdd(&a.recv[ev], cnt);  // (sent: derived, engine.hip)
+        if (t < 5u) sMisc[t] = 0ull;
+        sInc[er * 4u + 2u * ep] = n0;
+        sInc[er * 4u + 2u * ep + 1u] = n1;
+        __syncthreads();
+        DSTAMP(5);
+        // FT_next = new transposed (two 64 x 64 blocks per wave); liveness; the next tick's stage bit
+        unsigned long long any = 0ull;
+#pragma unroll
+        for (uint32_t q = 0; q < 2; q++) {
+            const uint32_t j = wid * 2u + q;
+            const uint32_t wi = j & 3u, rg = j >> 2;
+            const uint64_t x = sInc[(rg * 64u + lane) * 4u + wi];
+            const uint64_t col = wave_transpose64(x, lane);
+            const uint64_t c = (uint64_t)(w0 + wi) * 64u + lane;
+            *reinterpret_cast<uint64_t*>(a.FTn + c * a.kw + mblk * 8u + rg * 2u) = col;
+            const unsigned long long lv = __ballot(col != 0ull);
+            if (lane == 0 && lv) {
+                atomicOr(&sMisc[wi], lv);
+                any = 1ull;
+            }
+        }
+        if (lane == 0 && any) atomicOr(&sMisc[4], 1ull);
+        __syncthreads();
+        if (t < 4u) {
+            const unsigned long long x = sMisc[t];
+            if (x) atomicOr(&a.live[w0 + t], x);  // (no return: nothing waits for it)
+        } else if (t == 4u && sMisc[4]) {
+            const uint32_t stg = mblk >> 2;  // 4 row blocks of 256 per 1024-k stage
+            atomicOr(&a.snz_n[(uint64_t)ct * a.nstw + (stg >> 6)], 1ull << (stg & 63u));
+        }
+        __syncthreads();  // (sInc / sMisc reuse by the next tile)
+        DSTAMP(6);
+    };
+
+    // the first unit's stage goes out first, then the epilogue-only tiles -- active, no unit
+    // (nothing computed; F_next / FT_next zeroed, seen words of re-allocated words cleared),
+    // dealt round-robin -- run while it loads
     uint32_t buf = 0;
-    if (LT < thi) fused_issue(a, S, 0u, tile_mb(LT), tile_ct(LT), LS, wid, lane);
-
-    unsigned long long macs = 0, skipped = 0;
-    uint32_t t_srd = 0, t_swr = 0, t_fwr = 0;
-    unsigned long long snap_local = 0;
-
-    for (uint32_t T = tlo + bi; T < thi; T += bpx) {
-        const uint32_t mblk = tile_mb(T), ct = tile_ct(T), w0 = ct * 4u;
+    uint32_t LM = 0, LC = 0, LS = 0;
+    uint64_t LF = 0;
+    uint32_t rk = 0;
+    uint64_t rb = 0, re = 0;
+    bool have = range_of(0u, rb, re);
+    if (have) {
+        locate(rb, LM, LC, LS, LF);
+        fused_issue(a, S, 0u, LM, LC, LS, wid, lane);
+    }
+    DSTAMP(0);
+    for (uint32_t T = ord; T < a.total; T += G) {
+        const uint32_t ct = T % a.nt, mblk = T / a.nt;
+        if (!active(ct) || sCtU[ct] != 0u) continue;
+        const EpiIn in = epi_load(mblk, ct);
+        sInc[er * 4u + 2u * ep] = 0ull;
+        sInc[er * 4u + 2u * ep + 1u] = 0ull;
+        epilogue(mblk, ct, in);
+    }
+    DSTAMP(7);
+    // ---- this block's ranges, each a run of units [rb, re); the unit loads chain across them ----
+    uint64_t u = rb;
+    // A whole tile's epilogue is deferred to just after the next unit's barrier and before that
+    // unit's stage issue: its stores then have a whole unit of MFMA to complete before the next
+    // stage wait (vmcnt counts stores and atomics too: an epilogue right before a wait would hold
+    // every tile boundary for their acks)
+    bool pend = false;
+    uint32_t pM = 0, pC = 0;
+    EpiIn pin{};
+    while (have) {
+        // one tile segment: units [u, end) of tile (mblk, ct) -- the whole tile or a part of it
+        const uint32_t mblk = LM, ct = LC;
+        const uint64_t tfirst = LF, tlast = tfirst + sCtU[ct];
+        const uint64_t end = min<uint64_t>(re, tlast);
+        const uint64_t seg_b = max<uint64_t>(rb, tfirst);  // this block's first unit of the tile
+        const bool whole = seg_b == tfirst && end == tlast;
+        const uint32_t w0 = ct * 4u;
+        const uint64_t ev = (uint64_t)mblk * kDenseTile + er;
+        const uint32_t wa = w0 + 2u * ep;
         v16i_t acc[4][2];
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int j = 0; j < 2; j++) acc[i][j] = v16i_t{0};
-        uint32_t computed = 0;
-        // the own seen pair of this thread's row (prefetched with the tile's last stage)
-        const uint32_t er = t >> 1, ep = t & 1u;
-        const uint64_t ev = (uint64_t)mblk * kDenseTile + er;
-        const uint32_t wa = w0 + 2u * ep;
-        const uint32_t fa = a.wflags[wa], fb = a.wflags[wa + 1];
-        const uint64_t lpa = a.live_prev ? a.live_prev[wa] : ~0ull, lpb = a.live_prev ? a.live_prev[wa + 1] : ~0ull;
-        const bool dead = (lpa | lpb) == 0ull;
-        const bool need_seen = ev < a.n && (!dead || ((fa | fb) & WF_CLEAR));
-        ulonglong2 s2 = make_ulonglong2(0ull, 0ull);
-        bool seen_loaded = false;
-        while (LT == T) {  // the tile's stages, each already issued into `buf`
+        EpiIn ein{};
+        // after the segment: the next range when this one ends with it
+        bool next_have = true;
+        uint32_t next_k = rk;
+        uint64_t next_b = rb, next_e = re;
+        for (; u < end; u++) {
             const uint32_t s = LS;
-            // the next load: this tile's next stage, else the next tile with a stage
-            uint32_t nT = T, nS = s + 1u < a.nst ? first_stage(T, s + 1u) : a.nst;
-            if (nS >= a.nst) {
-                nT = T + bpx;
-                while (nT < thi && (nS = first_stage(nT, 0u)) >= a.nst) nT += bpx;
+            // the next unit: the tile's next stage, else the range's next column tile with units,
+            // else the first unit of the block's next range
+            uint32_t nM = LM, nC = LC, nS = a.nst;
+            uint64_t nF = LF;
+            bool more = true;
+            if (u + 1u < re) {
+                if (u + 1u < tlast) {
+                    nS = stage_from(LC, s + 1u);
+                } else {  // the next tile in tile order (one exists: u + 1 < re <= U)
+                    const uint32_t g = LM / GM;
+                    if (LM - g * GM + 1u < grows(g)) {
+                        nM = LM + 1u;
+                    } else {
+                        nM = g * GM;
+                        nC = LC + 1u;
+                        while (true) {
+                            if (nC >= a.nt) { nC = 0; nM += GM; }  // (the next group)
+                            if (sCtU[nC]) break;
+                            nC++;
+                        }
+                    }
+                    nF = tlast;
+                    nS = stage_from(nC, 0u);
+                }
+            } else {
+                more = false;
+                for (uint32_t k = rk + 1u; k <= R; k++) {
+                    uint64_t b, e;
+                    if (range_of(k, b, e)) {
+                        more = true;
+                        next_k = k;
+                        next_b = b;
+                        next_e = e;
+                        locate(b, nM, nC, nS, nF);
+                        break;
+                    }
+                }
+                next_have = more;
             }
+            DSTAMP(2);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();  // stage s landed for every wave; buffer buf ^ 1 is free
-            if (nT < thi) fused_issue(a, S, buf ^ 1u, tile_mb(nT), tile_ct(nT), nS, wid, lane);
-            if (nT != T && need_seen) {  // last stage of the tile: the epilogue's seen pair
-                s2 = *reinterpret_cast<const ulonglong2*>(a.seen + ev * a.stride + wa);
-                seen_loaded = true;
+            DSTAMP(1);
+            if (pend) {  // (no stage in flight: the epilogue's barriers drain nothing)
+                epilogue(pM, pC, pin);
+                pend = false;
             }
+            if (more) fused_issue(a, S, buf ^ 1u, nM, nC, nS, wid, lane);
+            if (u + 1u == end && whole) ein = epi_load(mblk, ct);  // the epilogue's inputs, early
             const uint8_t* As = S + buf * kFStageBytes;
             const uint8_t* Bs = As + kDenseTile * 128u;
 #pragma unroll
@@ -588,115 +966,98 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
                             acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i][j], 0, 0, 0);
                 }
             }
-            computed++;
+            macs++;
+            DSTAMP(2);
             buf ^= 1u;
-            LT = nT;
-            LS = nS;
+            LM = nM; LC = nC; LS = nS; LF = nF;
         }
-        if (need_seen && !seen_loaded) s2 = *reinterpret_cast<const ulonglong2*>(a.seen + ev * a.stride + wa);
-        macs += (unsigned long long)computed;
-        skipped += computed == 0u;
-        // ---- epilogue 1: Inc > 0 -> one 64-bit word per (row, word): wave ballots -> LDS ----
-        if (t < 5u) sMisc[t] = 0ull;
-        {
-            uint64_t lo = 0ull, hi = 0ull;
-            if (computed) {
+        // ---- Inc > 0 -> one 64-bit word per (row, word): wave ballots; lane l collects rows l (lo)
+        //      and l + 64 (hi) of the wave's 128 (a ballot of register g of MFMA tile (i, j) holds
+        //      columns 32j..32j+31 of row (g & 3) + 8 (g >> 2) in its low half, of the row 4 below in
+        //      its high half) ----
+        uint64_t lo = 0ull, hi = 0ull;
 #pragma unroll
-                for (int i = 0; i < 4; i++)
+        for (int i = 0; i < 4; i++)
 #pragma unroll
-                    for (int g = 0; g < 16; g++) {
-                        const unsigned long long q0 = __ballot(acc[i][0][g] > 0);
-                        const unsigned long long q1 = __ballot(acc[i][1][g] > 0);
-                        const uint64_t h0 = (q0 & 0xffffffffull) | (q1 << 32);
-                        const uint64_t h1 = (q0 >> 32) | (q1 & 0xffffffff00000000ull);
-                        const uint32_t row = (uint32_t)(i & 1) * 32u + (g & 3) + 8u * (g >> 2);
-                        if (i < 2) {
-                            if (lane == row) lo = h0;
-                            if (lane == row + 4u) lo = h1;
-                        } else {
-                            if (lane == row) hi = h0;
-                            if (lane == row + 4u) hi = h1;
-                        }
-                    }
+            for (int g = 0; g < 16; g++) {
+                const unsigned long long q0 = __ballot(acc[i][0][g] > 0);
+                const unsigned long long q1 = __ballot(acc[i][1][g] > 0);
+                const uint64_t h0 = (q0 & 0xffffffffull) | (q1 << 32);
+                const uint64_t h1 = (q0 >> 32) | (q1 & 0xffffffff00000000ull);
+                const uint32_t row = (uint32_t)(i & 1) * 32u + (g & 3) + 8u * (g >> 2);
+                if (i < 2) {
+                    if (lane == row) lo = h0;
+                    if (lane == row + 4u) lo = h1;
+                } else {
+                    if (lane == row) hi = h0;
+                    if (lane == row + 4u) hi = h1;
+                }
             }
+        DSTAMP(3);
+        const uint64_t vlo = (uint64_t)mblk * kDenseTile + wm * 128u + lane;
+        if (whole) {
             sInc[(wm * 128u + lane) * 4u + wn] = lo;
             sInc[(wm * 128u + 64u + lane) * 4u + wn] = hi;
-        }
-        __syncthreads();
-        // ---- epilogue 2: dedup of (row er, words wa, wa + 1) ----
-        {
-            uint64_t n0 = 0ull, n1 = 0ull;
-            if (ev < a.n) {
-                const uint64_t x0 = sInc[er * 4u + 2u * ep], x1 = sInc[er * 4u + 2u * ep + 1u];
-                if (fa & WF_CLEAR) s2.x = 0ull;
-                if (fb & WF_CLEAR) s2.y = 0ull;
-                const uint64_t k0 = (fa & WF_KEEP) ? a.ctl[wa].keep : ~0ull;
-                const uint64_t k1 = (fb & WF_KEEP) ? a.ctl[wa + 1].keep : ~0ull;
-                n0 = x0 & ~s2.x & k0;
-                n1 = x1 & ~s2.y & k1;
-                const bool swr = (n0 | n1) != 0ull || ((fa | fb) & WF_CLEAR) != 0u;
-                if (swr) *reinterpret_cast<ulonglong2*>(a.seen + ev * a.stride + wa) = make_ulonglong2(s2.x | n0, s2.y | n1);
-                *reinterpret_cast<ulonglong2*>(a.Fnext + ev * a.stride + wa) = make_ulonglong2(n0, n1);
-                t_srd += need_seen;
-                t_swr += swr;
-                t_fwr += 1u;
-                if (a.snap) {
-                    if (fa & WF_SNAP) snap_local += (unsigned long long)__popcll(n0 & a.ctl[wa].snap);
-                    if (fb & WF_SNAP) snap_local += (unsigned long long)__popcll(n1 & a.ctl[wa + 1].snap);
-                }
-                // tile occupancy of F_next: every tile row of the window is written (zeros included)
-                if (ct == 0u && ep == 0u) {
-                    const uint32_t ntl = a.wact / 16u;
-                    for (uint32_t j = 0; j < a.ntw; j++) {
-                        const uint32_t lo_t = j * 64u;
-                        const unsigned long long m = ntl <= lo_t ? 0ull : ntl - lo_t >= 64u ? ~0ull : ((1ull << (ntl - lo_t)) - 1ull);
-                        a.nz_next[ev * a.ntw + j] = m;
-                    }
-                }
+            pend = true;  // (the next unit's barrier orders these writes before the epilogue)
+            pM = mblk;
+            pC = ct;
+            pin = ein;
+        } else {
+            // a split tile: OR the partial words into inc, count the units into the tile's ticket;
+            // the block completing it takes the words back and runs the epilogue
+            unsigned long long* ip = a.inc + vlo * a.stride + w0 + wn;
+            if (lo && vlo < a.n) atomicOr(ip, (unsigned long long)lo);
+            if (hi && vlo + 64u < a.n) atomicOr(ip + 64ull * a.stride, (unsigned long long)hi);
+            __syncthreads();  // (every wave's atomics done: vmcnt(0) before the barrier)
+            if (t == 0) {
+                const uint32_t mineu = (uint32_t)(end - seg_b);  // units this block reduced into the tile
+                const uint32_t T = mblk * a.nt + ct;
+                const uint32_t old = __hip_atomic_fetch_add(&a.tix[T], mineu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const bool last = old + mineu == sCtU[ct];
+                if (last) __hip_atomic_store(&a.tix[T], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                sMisc[5] = last ? 1ull : 0ull;
             }
-            uint32_t cnt = (uint32_t)(__popcll(n0) + __popcll(n1));
-            cnt += (uint32_t)__shfl_xor((int)cnt, 1, 64);
-            if (ep == 0u && cnt) atomicAdd(&a.recv[ev], cnt);  // (sent: derived, engine.hip)
-            sInc[er * 4u + 2u * ep] = n0;
-            sInc[er * 4u + 2u * ep + 1u] = n1;
-        }
-        __syncthreads();
-        // ---- epilogue 3: FT_next = new transposed; liveness; the next tick's stage bit ----
-        {
-            unsigned long long any = 0ull;
-#pragma unroll
-            for (uint32_t q = 0; q < 2; q++) {
-                const uint32_t j = wid * 2u + q;         // 64 x 64 block j of the tile's 16
-                const uint32_t wi = j & 3u, rg = j >> 2;  // word, 64-row group
-                const uint64_t x = sInc[(rg * 64u + lane) * 4u + wi];
-                const uint64_t col = wave_transpose64(x, lane);
-                const uint64_t c = (uint64_t)(w0 + wi) * 64u + lane;
-                *reinterpret_cast<uint64_t*>(a.FTn + c * a.kw + mblk * 8u + rg * 2u) = col;
-                const unsigned long long lv = __ballot(col != 0ull);
-                if (lane == 0 && lv) {
-                    atomicOr(&sMisc[wi], lv);
-                    any = 1ull;
+            __syncthreads();
+            DSTAMP(4);
+            if (sMisc[5]) {
+                // (atomic exchange: the other blocks' atomics are read where they were performed)
+                if (ev < a.n) {
+                    unsigned long long* rp = a.inc + ev * a.stride + wa;
+                    sInc[er * 4u + 2u * ep] = atomicExch(rp, 0ull);
+                    sInc[er * 4u + 2u * ep + 1u] = atomicExch(rp + 1, 0ull);
+                } else {
+                    sInc[er * 4u + 2u * ep] = 0ull;
+                    sInc[er * 4u + 2u * ep + 1u] = 0ull;
                 }
+                const EpiIn in = epi_load(mblk, ct);
+                __syncthreads();
+                epilogue(mblk, ct, in);
             }
-            if (lane == 0 && any) atomicOr(&sMisc[4], 1ull);
         }
+        if (u == re) {  // the range is done: on to the next one (its first unit is already loading)
+            have = next_have;
+            rk = next_k;
+            rb = next_b;
+            re = next_e;
+            u = rb;
+        }
+    }
+    if (pend) {  // the last tile's epilogue
         __syncthreads();
-        if (t < 4u) {
-            const unsigned long long x = sMisc[t];
-            if (x) {
-                const unsigned long long have = __hip_atomic_load(&a.live[w0 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (x & ~have) atomicOr(&a.live[w0 + t], x);
-            }
-        } else if (t == 4u && sMisc[4]) {
-            const uint32_t st = mblk >> 2;  // 4 row blocks of 256 per 1024-k stage
-            atomicOr(&a.snz_n[(uint64_t)ct * a.nstw + (st >> 6)], 1ull << (st & 63u));
-        }
-        // (the next tile's first barrier orders sInc / sMisc reuse)
+        epilogue(pM, pC, pin);
     }
     if (a.snap) {
         snap_local = wave_sum(snap_local);
         if (lane == 0 && snap_local) atomicAdd(a.snap, snap_local);
     }
+#ifdef DENSE_STAMPS
+    if (a.acct && lane == 0)
+        for (int k = 0; k < 8; k++) acct_add(a.acct, 22u + (uint32_t)k, (unsigned long long)dcyc[k]);
+    if (a.acct && t == 0) {  // block 0..G-1 durations: realtime ticks, shader cycles (wave 0)
+        acct_add(a.acct, 30u, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - drt0));
+        acct_add(a.acct, 31u, (unsigned long long)(__builtin_amdgcn_s_memtime() - dmt0));
+    }
+#endif
     if (a.acct) {
         const uint32_t tv[3] = {(uint32_t)wave_sum(t_srd), (uint32_t)wave_sum(t_swr), (uint32_t)wave_sum(t_fwr)};
         if (lane == 0) {
@@ -705,6 +1066,10 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
                 if (tv[q]) acct_add(a.acct, 2 + q, (unsigned long long)tv[q]);
         }
         if (t == 0 && macs) acct_add(a.acct, 5, 2ull * kDenseTile * kDenseTile * kStageK * macs);
-        if (t == 0 && skipped) acct_add(a.acct, 6, skipped);
+        if (t == 0 && ord == 0) {  // tiles computing nothing (no live word or no non-empty stage)
+            uint32_t z = 0;
+            for (uint32_t c = 0; c < a.nt; c++) z += sCtU[c] == 0u;
+            if (z) acct_add(a.acct, 6, (unsigned long long)z * a.mb);
+        }
     }
 }

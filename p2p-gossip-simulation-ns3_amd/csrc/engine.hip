@@ -695,7 +695,10 @@ struct gossip_engine {
     uint32_t snz_nstw = 0;              // mask words per column tile
     bool ft_valid = false;              // d_FT[fcur] / d_snz[fcur] were written by the fused path
     int64_t opt_dense_fused = 1;        // 1: k_dense_fused when the tick allows it (tick_step_a)
+    int64_t dense_rounds = -1;          // k_dense_fused's most data-parallel rounds (A/B env GOSSIP_DENSE_ROUNDS; -1: all)
+    int64_t dense_gm = 4;               // k_dense_fused's row blocks per tile group (A/B env GOSSIP_DENSE_GM)
     uint64_t fused_launches = 0;
+    uint32_t* d_tix = nullptr;          // fused path: per-tile tickets of split tiles (n_pad / 256 x stride / 4)
     unsigned long long* d_inc = nullptr;  // n x stride incoming words (GEMM -> pull)
     uint32_t *d_recv = nullptr, *d_gen = nullptr, *d_effgen = nullptr;
     uint64_t* d_sent = nullptr;
@@ -901,7 +904,7 @@ gossip_engine::~gossip_engine() {
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
     hipFree(d_rowptr_c); hipFree(d_col_c); hipFree(d_degc);
     for (int k = 0; k < 4; k++) { hipFree(d_smask[k]); hipHostFree(h_smask[k]); }
-    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen_mem); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_sat); hipFree(d_Ab); hipFree(d_FT[0]); hipFree(d_FT[1]); hipFree(d_snz[0]); hipFree(d_snz[1]); hipFree(d_snz[2]); hipFree(d_inc);
+    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen_mem); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_sat); hipFree(d_Ab); hipFree(d_FT[0]); hipFree(d_FT[1]); hipFree(d_snz[0]); hipFree(d_snz[1]); hipFree(d_snz[2]); hipFree(d_tix); hipFree(d_inc);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent); hipFree(d_phase_ts);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     hipFree(d_msg); hipFree(d_cnt); hipFree(d_scan_tmp); hipFree(d_recv_msgs); hipFree(d_sizes);
@@ -1325,7 +1328,10 @@ int gossip_engine::alloc_device() {
         ft_valid = false;
         HIP_TRY(hipMalloc(&d_inc, bm));
         HIP_TRY(hipMemsetAsync(d_inc, 0, bm, stream));
-        device_bytes += 2 * ft + 3 * snzb + bm + (uint64_t)n_pad * n_pad / 8;
+        const uint64_t tixb = (uint64_t)(n_pad / kDenseTile) * (stride / 4u) * 4u;
+        HIP_TRY(hipMalloc(&d_tix, tixb));
+        HIP_TRY(hipMemsetAsync(d_tix, 0, tixb, stream));
+        device_bytes += 2 * ft + 3 * snzb + bm + tixb + (uint64_t)n_pad * n_pad / 8;
     }
     if (batch && !snaps.empty())
         for (int k = 0; k < kRing; k++) {
@@ -1464,6 +1470,11 @@ int gossip_engine::grow(uint32_t new_stride) {
         d_inc = nullptr;
         HIP_TRY(hipMalloc(&d_inc, nb));
         HIP_TRY(hipMemset(d_inc, 0, nb));
+        HIP_TRY(hipFree(d_tix));
+        d_tix = nullptr;
+        const uint64_t tixb = (uint64_t)(n_pad / kDenseTile) * (new_stride / 4u) * 4u;
+        HIP_TRY(hipMalloc(&d_tix, tixb));
+        HIP_TRY(hipMemset(d_tix, 0, tixb));
         device_bytes += (uint64_t)(new_stride - stride) * (16ull * n_pad + 8ull * n + 6ull * snz_nstw);
     }
     if (batch && !snaps.empty())
@@ -1853,6 +1864,8 @@ int gossip_engine::tick_step_a(int64_t t) {
         if (YP->yt[i].flags)
             for (uint32_t q = 0; q < kTileWords; q++) WF[YP->yt[i].tile * kTileWords + q] |= (uint8_t)WF_YOUNG;
     for (uint32_t w : reset_now) ctl[w].clear = 0ull;
+    for (uint32_t q = 0; q < nb; q++)  // (k_dense_fused writes the 16-word tiles births land in)
+        if (B[q].kind == BIRTH_NORMAL || B[q].kind == BIRTH_GROUP) WF[B[q].col >> 6] |= (uint8_t)WF_BIRTH;
     // 4b. k_pull's pass -> tile lists (option pull_tiles), one per launch window: the allocated,
     //     non-young tiles, grouped by occupancy word and padded to whole passes of LPW / 8 tiles
     //     (LPW as run_pull picks it below).  Young tiles are k_pull_young's, retired tiles hold
@@ -1981,7 +1994,8 @@ int gossip_engine::tick_step_a(int64_t t) {
     // DENSE ticks run k_dense_fused (dense_kernel.h) unless the tick has id groups, row chunks
     // (row partition: other ranks' rows reach F_next without FT), or the diagnostic no-skip pull
     const bool fused_tick = dense && wact && opt_dense_fused && nchunks == 1 && row_count == 1 &&
-                            !(cfg.flags & GOSSIP_F_NOSKIP) && !group_any;
+                            !(cfg.flags & GOSSIP_F_NOSKIP) && !group_any && ntw <= kFActWords &&
+                            (uint64_t)(wact / 4u) * (n_pad / kStageK) < (1ull << 20);  // (its packed unit scan)
     // births [off, off + cnt) of the staged array (all of them, or one row chunk's)
     auto launch_births = [&](uint32_t off, uint32_t cnt) -> int {
         if (!cnt) return GOSSIP_OK;
@@ -2096,16 +2110,19 @@ int gossip_engine::tick_step_a(int64_t t) {
         // (k_phase_start, k_phase_acc): an event pair around the phase also counted the host's
         // launch latency (273 us against a 136 us span on C2, profiles/r04).
         unsigned long long* pts = dense_timing ? d_phase_ts : nullptr;
-        // a fused tick after a three-kernel one: the stage masks it writes were not zeroed
+        // a fused tick after a three-kernel one: the stage masks it writes were not zeroed, and
+        // k_transpose builds the ones it reads
         if (fused_tick && !ft_valid)
-            HIP_TRY(hipMemsetAsync(d_snz[(t + 1) % 3], 0, (size_t)(stride / 4u) * snz_nstw * 8u, stream));
+            for (int64_t k = 0; k < 2; k++)
+                HIP_TRY(hipMemsetAsync(d_snz[(t + k) % 3], 0, (size_t)(stride / 4u) * snz_nstw * 8u, stream));
         if (pts) k_phase_start<<<1, 1, 0, stream>>>(pts);
         if (dense && !(fused_tick && ft_valid)) {
             // transpose the frontier to share-column bit rows (the fused path's FT[fcur] was
             // written by the last tick's k_dense_fused + k_births)
             dim3 eg(n_pad / 256u, wact);
             k_transpose<<<eg, 256, 0, stream>>>(d_F[fcur], stride, n, n_pad / 32u, wact, a.live_prev,
-                                                d_nz[fcur], ntw, d_FT[fcur]);
+                                                d_nz[fcur], ntw, d_FT[fcur], fused_tick ? d_snz[t % 3] : nullptr,
+                                                snz_nstw);
             HIP_TRY(hipGetLastError());
         }
         // young tiles beside k_pull: the two kernels touch disjoint words; they share the per-node
@@ -2241,7 +2258,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             // the whole DENSE pull in one persistent kernel (contraction, dedup, FT of F_next)
             FusedArgs f;
             f.Ab = d_Ab; f.FTc = d_FT[fcur]; f.FTn = d_FT[nxt];
-            f.snz_c = ft_valid ? d_snz[t % 3] : nullptr;
+            f.snz_c = d_snz[t % 3];  // (by the last tick's fused kernel + births, or k_transpose above)
             f.snz_n = d_snz[(t + 1) % 3];
             f.snz_z = d_snz[(t + 2) % 3];
             f.snz_zwords = (stride / 4u) * snz_nstw;
@@ -2252,6 +2269,10 @@ int gossip_engine::tick_step_a(int64_t t) {
             f.nst = n_pad / kStageK; f.nstw = snz_nstw;
             f.mb = n_pad / kDenseTile; f.nt = wact / 4u; f.total = f.mb * f.nt;
             f.wact = wact;
+            f.inc = d_inc;
+            f.tix = d_tix;
+            f.rmax = dense_rounds < 0 ? 0xffffffffu : (uint32_t)dense_rounds;
+            f.gm = (uint32_t)std::min<int64_t>(dense_gm, 64);
             uint32_t fg = (uint32_t)std::min<uint64_t>(f.total, (uint64_t)num_cus);
             if (fg >= 8u) fg &= ~7u;
             k_dense_fused<<<fg, 512, 0, stream>>>(f);
@@ -2983,6 +3004,8 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_pull_grid = env_option("GOSSIP_PULL_GRID", 0);
         e->opt_dense_min_tiles = env_option("GOSSIP_DENSE_MIN_TILES", 512);
         e->opt_dense_fused = env_option("GOSSIP_DENSE_FUSED", 1);
+        e->dense_rounds = env_option("GOSSIP_DENSE_ROUNDS", -1);
+        e->dense_gm = std::max<int64_t>(1, env_option("GOSSIP_DENSE_GM", 4));
         e->opt_young = env_option("GOSSIP_YOUNG", -1);
         e->opt_young_age = env_option("GOSSIP_YOUNG_AGE", 5);
         e->opt_young_cap = env_option("GOSSIP_YOUNG_CAP", 127);
@@ -3848,6 +3871,11 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
                            5ull * acct[9] +
                            8ull * (acct[11] + acct[12]) + e->young_launches * (8ull * (e->n + 1) + 16ull * e->n);
     c->young_fresh_lines = acct[19];
+#ifdef DENSE_STAMPS
+    fprintf(stderr, "dense_stamps_cycles");
+    for (int k = 22; k < 32; k++) fprintf(stderr, " %llu", (unsigned long long)acct[k]);  // (30, 31: block time)
+    fprintf(stderr, "\n");
+#endif
 #ifdef YOUNG_STAMPS
     fprintf(stderr, "young_stamps_cycles");
     for (int k = 22; k < 30; k++) fprintf(stderr, " %llu", (unsigned long long)acct[k]);  // (20, 21: k_pull items)

@@ -103,7 +103,7 @@ __device__ __forceinline__ uint32_t group_add(uint32_t x, uint32_t lane) {
 // WF_DW: write every node's F_next row of the tile, zeros included (its readers of the next tick
 //        read it without occupancy words: dense rows, above)
 enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u, WF_YOUNG = 16u, WF_LATE = 32u,
-                  WF_DW = 64u };
+                  WF_DW = 64u, WF_BIRTH = 128u };  // WF_BIRTH: a generation lands in the word this tick (k_dense_fused)
 // PullArgs::tmask, per occupancy word tw: [3 tw] dense-row tiles (read without occupancy words),
 // [3 tw + 1] tiles whose sat bits are trusted this tick, [3 tw + 2] listed tiles that need occupancy
 enum : uint32_t { TM_DENSE = 0, TM_SATOK = 1, TM_NZ = 2, TM_WORDS = 3 };

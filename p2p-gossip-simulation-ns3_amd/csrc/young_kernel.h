@@ -179,6 +179,18 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
     } while (0)
 #endif
 
+// Measurement build YOUNG_DUP=k (tools/ab: instruction counts per segment by PMC): segment k of the
+// node loop runs twice on the same data -- the first launch's count difference is its cost.  Its
+// outputs are wrong by design (counters double); never a product build.
+#ifndef YOUNG_DUP
+#define YOUNG_DUP 0
+#endif
+#if YOUNG_DUP
+#define YDUP(k) for (int ydup_ = 0; ydup_ < (YOUNG_DUP == (k) ? 2 : 1); ydup_++)
+#else
+#define YDUP(k)  // (the product build: no wrapper at all -- a one-trip loop still moved register allocation)
+#endif
+
 // 256-thread blocks; the register budget of 4 waves per SIMD (A/B build: YOUNG_MIN_WAVES)
 #ifndef YOUNG_MIN_WAVES
 #define YOUNG_MIN_WAVES 4
@@ -346,7 +358,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             const int32_t np0 = min(64, end - beg);
             t_col += (uint32_t)max(0, end - beg);
             unsigned long long ovf = 0ull;
-            issue(cid_cur, 0);
+            YDUP(7) issue(cid_cur, 0);
             // own seen list (its two lines, 2 entries per lane), with the first batch
             const uint32_t ql = reinterpret_cast<const uint32_t*>(a.list + v * kListU16)[lane];
             t_lr += 2u;
@@ -354,7 +366,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             int32_t rv_next = -1;
             const uint32_t cid_next = load_ids(jn + 1u, h_next, rv_next);  // the next node's peers
             YSTAMP(0);
-            consume(cid_cur, 0, np0, ovf);
+            YDUP(1) consume(cid_cur, 0, np0, ovf);
             for (int32_t pb = 8 * kYoungQ; pb < np0; pb += 8 * kYoungQ) {  // degree > 8 kYoungQ
                 issue(cid_cur, pb);
                 consume(cid_cur, pb, np0, ovf);
@@ -388,7 +400,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             uint32_t keepm = 0u;  // bit j: entry j is kept into the new list (its tile stays young)
             reinterpret_cast<uint32_t*>(s_lst)[lane] = 0xffffffffu;  // tombstones
             __builtin_amdgcn_wave_barrier();
-            if (!lovf) {
+            YDUP(2) if (!lovf) {
 #pragma unroll
                 for (uint32_t j = 0; j < 2u; j++) {
                     const uint32_t e = lentry(j);
@@ -414,7 +426,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             __builtin_amdgcn_wave_barrier();
             // ---- touched words -> list ----
             uint32_t ntouch = 0;
-            for (uint32_t i0 = 0; i0 < nrw; i0 += 64) {
+            YDUP(3) for (uint32_t i0 = (ntouch = 0u); i0 < nrw; i0 += 64) {
                 const uint32_t i = i0 + lane;
                 const bool hit = i < nrw && s_acc[i] != 0ull;
                 const unsigned long long m = __ballot(hit);
@@ -468,8 +480,22 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
                         const uint32_t pk = (cl << 16) | cs, incl = wave_incl_scan(pk), ex = incl - pk;
                         uint32_t ps = 1u + slot_total + (ex & 0xffffu), pl = total + (ex >> 16);
                         const uint32_t tot = lane_read(incl, 63u);
+                        // (uniform) every lane's list bits are its slot bits (no id group among the
+                        // words): one pass writes both entries, the list's at a uniform offset
+                        const bool same = !LO && !__ballot(xl != (cs ? x : 0ull));
+                        const uint32_t dl = total - 1u - slot_total;
                         slot_total += tot & 0xffffu;
                         total += tot >> 16;
+                        if (same) {
+                            const uint32_t sb = ((uint32_t)yt.w_idx << 10) | ((i & 15u) << 6);
+                            const uint32_t lb = ((uint32_t)yt.yid << 10) | ((i & 15u) << 6);
+                            for (uint64_t m = xl; m; m &= m - 1ull, ps++) {
+                                const uint32_t bit = (uint32_t)__builtin_ctzll(m);
+                                if (ps < kSlotU16) s_out[ps] = (uint16_t)(sb | bit);
+                                if (ps + dl < kListU16) s_lst[ps + dl] = (uint16_t)(lb | bit);
+                            }
+                            continue;
+                        }
                         for (uint64_t m = cs ? x : 0ull; m; m &= m - 1ull, ps++)
                             if (ps < kSlotU16)
                                 s_out[ps] = (uint16_t)(((uint32_t)yt.w_idx << 10) | ((i & 15u) << 6) | (uint32_t)__builtin_ctzll(m));
@@ -479,10 +505,20 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
                     }
                 }
             };
-            if (lovf)
-                dedup(std::true_type{});
-            else
-                dedup(std::false_type{});
+#if YOUNG_DUP
+            const uint32_t ydc = cnt, yds = slot_total, ydt = total;
+#endif
+            YDUP(4) {
+#if YOUNG_DUP
+                cnt = ydc;  // (a repeated pass starts from the same state: same outputs)
+                slot_total = yds;
+                total = ydt;
+#endif
+                if (lovf)
+                    dedup(std::true_type{});
+                else
+                    dedup(std::false_type{});
+            }
             const uint32_t lcount = total - 1u;
             const bool lspill = !lovf && lcount > a.list_cap;  // (uniform) the list overflows now
             __builtin_amdgcn_wave_barrier();
@@ -497,7 +533,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             uint16_t* out = a.slot_next + v * kSlotU16;
             if (lane == 0) s_out[0] = (uint16_t)(overflow ? kSlotOverflow : slot_total);
             __builtin_amdgcn_wave_barrier();
-            {
+            YDUP(5) {
                 const uint32_t lines = (!overflow && slot_total > 63u) ? 2u : 1u;
                 if (lane < 8u * lines)
                     *reinterpret_cast<ulonglong2*>(out + lane * 8u) = *reinterpret_cast<const ulonglong2*>(s_out + lane * 8u);
@@ -516,7 +552,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             const uint32_t ndense = overflow ? a.ny : a.nt;
             unsigned long long nzw = 0ull;
             uint32_t nz_tw = 0xffffffffu;
-            for (uint32_t q0 = 0; q0 < ndense; q0 += 4) {
+            YDUP(6) for (uint32_t q0 = 0; q0 < ndense; q0 += 4) {
                 const uint32_t qi = q0 + (lane >> 4), word = lane & 15u;
                 const bool in = qi < ndense;
                 const uint32_t q = !in ? 0u : overflow ? qi : (uint32_t)s_lv[qi];
