@@ -313,10 +313,11 @@ def main():
     ap.add_argument("--rehearse-shards", type=int, default=0,
                     help="diagnostic: run only shard 0 of S on this one GPU (per-rank footprint "
                          "and time of an S-GPU run); the JSON line is marked REHEARSAL")
-    ap.add_argument("--shard-rule", choices=["hash", "tick"], default="hash",
-                    help="share-shard rule: hash of the instance key (default) or the birth tick of "
-                         "its first generation (GOSSIP_F_SHARD_BY_TICK: a shard's births of a tick "
-                         "fill whole tiles of one age)")
+    ap.add_argument("--shard-rule", choices=["auto", "hash", "tick"], default="auto",
+                    help="share-shard rule: hash of the instance key, or the birth tick of its first "
+                         "generation (GOSSIP_F_SHARD_BY_TICK: a shard's births of a tick fill whole "
+                         "tiles of one age); auto (default): tick from 8 shards on, hash below "
+                         "(DESIGN.md section 5: measured one-rank rehearsals)")
     ap.add_argument("--rehearse-rows", type=int, default=0,
                     help="diagnostic: one rank of an R-rank row partition of share shard 0 of "
                          "--rehearse-shards (default: the workload's fit) on this one GPU")
@@ -361,8 +362,10 @@ def main():
     t_gen_end = SLICE_NS + (W + K + 1) * L_NS
     ev, sinfo = WL.slice_schedule(n, WL.CONFIGS[args.workload]["node_seed"], SLICE_NS, t_gen_end,
                                   threads=args.threads)
-    flags = gossip.F_TIMING | (gossip.F_NOSKIP if args.noskip else 0) | \
-        (gossip.F_SHARD_BY_TICK if args.shard_rule == "tick" else 0)
+    flags = gossip.F_TIMING | (gossip.F_NOSKIP if args.noskip else 0)
+
+    def shard_rule(shards):
+        return args.shard_rule if args.shard_rule != "auto" else ("tick" if shards >= 8 else "hash")
     if rank == 0:
         rp, _, _ = topo.csr()
         log(f"[bench] {wl['desc']}: {topo.num_nodes} nodes, {int(rp[-1])} directed entries, "
@@ -384,7 +387,8 @@ def main():
             shards, my_shards = args.rehearse_shards * (passes // max(1, -(-wl["fit_shards"] // world))), [0]
         err = None
         try:
-            acc = run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, flags)
+            acc = run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank,
+                             flags | (gossip.F_SHARD_BY_TICK if shard_rule(shards) == "tick" else 0))
         except gossip.GossipError as e:
             if getattr(e, "code", None) not in CAPACITY_CODES:
                 raise
@@ -459,7 +463,7 @@ def main():
                 "window_early_retires": acc.get("early_retires", 0),
                 "device_gib": acc["dev_bytes"] / 2**30,
                 "parallelism": f"share-shard x{shards} over {max(world, 1)} rank(s)",
-                "shard_rule": args.shard_rule,
+                "shard_rule": shard_rule(shards),
             },
             "roofline": None,
         }

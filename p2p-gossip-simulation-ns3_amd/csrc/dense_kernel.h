@@ -434,12 +434,14 @@ struct FusedArgs {
 constexpr uint32_t kFStageBytes = 2u * kDenseTile * 128u;  // A + B rows of one 1024-k stage
 constexpr uint32_t kFIncOff = 2u * kFStageBytes;           // 256 rows x 4 words of inc / new
 constexpr uint32_t kFMiscOff = kFIncOff + kDenseTile * 4u * 8u;
-constexpr uint32_t kFActWords = 8;                          // active-tile bits: windows <= 8,192 words
+constexpr uint32_t kFActWords = 4;                          // active-tile bits: windows <= 4,096 words
 constexpr uint32_t kFActOff = kFMiscOff + 64u;
 constexpr uint32_t kFMaxCt = kFActWords * 64u * 4u;         // column tiles of the widest window
 constexpr uint32_t kFCtOff = kFActOff + kFActWords * 8u;    // per column tile: units, prefix (u32)
 constexpr uint32_t kFLctOff = kFCtOff + 2u * kFMaxCt * 4u;  // the column tiles with units, in order (u16)
-constexpr uint32_t kFLdsBytes = kFLctOff + kFMaxCt * 2u;
+constexpr uint32_t kFFlgOff = kFLctOff + kFMaxCt * 2u;      // per column tile: its 4 word-flag bytes
+constexpr uint32_t kFS2Off = (kFFlgOff + kFMaxCt * 4u + 15u) & ~15u;  // the epilogue's seen pairs (LDS-DMA)
+constexpr uint32_t kFLdsBytes = kFS2Off + 512u * 16u;
 static_assert(kFLdsBytes <= 163840u, "k_dense_fused LDS");
 static_assert(kStageK == 1024u, "k_dense_fused stages 128-B rows");
 
@@ -537,10 +539,45 @@ __device__ __forceinline__ uint64_t wave_transpose64(uint64_t x, uint32_t lane) 
     return x;
 }
 
+// Lanes L and L + 4 of the pair (x0, x1) := (a0, a1) and (b0, b1) (wave-uniform SGPR values):
+// v_writelane (one VALU each, EXEC ignored).  The row words of the fused epilogue's ballots are
+// placed this way: the select form (lane == row ? h : x) cost a compare, SGPR->VGPR moves and
+// lane-mask reloads per row (hipcc has no writelane builtin).  The s_nop keeps the writelanes 5
+// wait states behind the compares that wrote their SGPRs (without it, bits were lost).
+template <int L>
+__device__ __forceinline__ void write_lanes(uint32_t& x0, uint32_t& x1, uint32_t a0, uint32_t a1, uint32_t b0,
+                                            uint32_t b1) {
+    asm volatile(
+        "s_nop 4\n\t"
+        "v_writelane_b32 %0, %2, %6\n\t"
+        "v_writelane_b32 %1, %3, %6\n\t"
+        "v_writelane_b32 %0, %4, %7\n\t"
+        "v_writelane_b32 %1, %5, %7"
+        : "+v"(x0), "+v"(x1)
+        : "s"(a0), "s"(a1), "s"(b0), "s"(b1), "n"(L), "n"(L + 4));
+}
+// Inc > 0 -> row words: ballot of MFMA register g of tiles (i, 0) and (i, 1) = row (g & 3) + 8 (g >> 2)
+// (+ 32 for odd i) in its low half, the row 4 below in its high half; w[0..1] = lo (rows 0..63 of
+// the wave), w[2..3] = hi (rows 64..127), low / high 32 columns
+template <int K>
+__device__ __forceinline__ void fused_row_words(const v16i_t (&acc)[4][2], uint32_t (&w)[4]) {
+    if constexpr (K < 64) {
+        constexpr int i = K / 16, g = K % 16;
+        constexpr int row = (i & 1) * 32 + (g & 3) + 8 * (g >> 2);
+        constexpr int d = i < 2 ? 0 : 2;
+        const unsigned long long q0 = __ballot(acc[i][0][g] > 0);
+        const unsigned long long q1 = __ballot(acc[i][1][g] > 0);
+        write_lanes<row>(w[d], w[d + 1], (uint32_t)q0, (uint32_t)q1, (uint32_t)(q0 >> 32), (uint32_t)(q1 >> 32));
+        fused_row_words<K + 1>(acc, w);
+    }
+}
+
 // Diagnostic build DENSE_STAMPS: shader cycles per phase of k_dense_fused (s_memtime), summed over
-// waves into acct[22..29] (engine.hip prints them); no output depends on them.  0 prologue, 1 stage
-// wait + barrier, 2 stage issue + MFMA, 3 ballots, 4 split-tile reduction, 5 epilogue dedup,
-// 6 epilogue transpose + liveness, 7 epilogue-only tiles
+// waves into acct[22..29] (engine.hip prints them); no output depends on them.  0 prologue and
+// epilogue-only tiles, 1 stage barrier (waves waiting for each other), 2 stage issue + MFMA,
+// 3 ballots, 4 split-tile reduction, 5 epilogue dedup, 6 epilogue transpose + liveness, 7 the
+// wave's own stage wait (vmcnt: its DMA pieces, and stores of a deferred epilogue); acct[30]
+// block time (s_memrealtime, 100 MHz) and acct[31] its shader cycles, per block
 #ifdef DENSE_STAMPS
 #define DSTAMP(k)                                              \
     do {                                                       \
@@ -567,6 +604,8 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
     uint32_t* sCtU = reinterpret_cast<uint32_t*>(S + kFCtOff);  // units of column tile ct (any row block)
     uint32_t* sCtP = sCtU + kFMaxCt;                             // exclusive prefix of sCtU
     uint16_t* sLct = reinterpret_cast<uint16_t*>(S + kFLctOff);  // column tiles with units, in order
+    uint32_t* sCtF = reinterpret_cast<uint32_t*>(S + kFFlgOff);  // the column tile's word flags
+    const ulonglong2* sS2 = reinterpret_cast<const ulonglong2*>(S + kFS2Off);  // thread t's seen pair
     const uint32_t t = threadIdx.x, lane = t & 63u, wid = wave_in_block();
     const uint32_t wm = wid >> 2, wn = wid & 3u;
     for (uint32_t i = blockIdx.x * 512u + t; i < a.snz_zwords; i += gridDim.x * 512u) a.snz_z[i] = 0ull;
@@ -598,6 +637,7 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
         if (in) {
             if ((ct & 3u) == 0u && c) atomicOr(&sAct[ct >> 8], 1ull << ((ct >> 2) & 63u));
             sCtU[ct] = (c && lp != 0ull) ? u : 0u;
+            sCtF[ct] = f;
         }
     }
     __syncthreads();
@@ -728,6 +768,14 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
         }
         return a.nst;
     };
+    // one-word stage masks (nst <= 64 stages): the current tile's mask stays in a register, so the
+    // next unit of the same tile needs no load (a load there waited at every unit: vmcnt(0))
+    const bool one_word = a.nstw == 1u;
+    auto stage_in = [&](uint64_t m, uint32_t from) -> uint32_t {
+        if (from >= a.nst) return a.nst;
+        m >>= from;
+        return m ? from + (uint32_t)__builtin_ctzll(m) : a.nst;
+    };
     // unit u -> (row block, column tile, stage); also the tile's first unit
     auto locate = [&](uint64_t u, uint32_t& mblk, uint32_t& ct, uint32_t& st, uint64_t& tfirst) {
         const uint32_t g = (uint32_t)(u / GU), rows = grows(g);
@@ -749,30 +797,23 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
 
     // ---- the epilogue's per-thread inputs (row er, words wa, wa + 1 of tile (mblk, ct)), loaded
     //      with no dependence between them -- one round trip, issued with the tile's last stage ----
-    struct EpiIn {
-        uint32_t fa, fb;
-        uint64_t lpa, lpb;
-        ulonglong2 s2;
-    };
-    auto epi_load = [&](uint32_t mblk, uint32_t ct) -> EpiIn {
-        EpiIn e;
-        const uint32_t wa = ct * 4u + 2u * ep;
-        const uint64_t ev = (uint64_t)mblk * kDenseTile + er;
-        e.fa = a.wflags[wa];
-        e.fb = a.wflags[wa + 1];
-        e.lpa = a.live_prev ? a.live_prev[wa] : ~0ull;
-        e.lpb = a.live_prev ? a.live_prev[wa + 1] : ~0ull;
-        e.s2 = ev < a.n ? *reinterpret_cast<const ulonglong2*>(a.seen + ev * a.stride + wa) : make_ulonglong2(0ull, 0ull);
-        return e;
+    //      (the own seen pairs go to LDS by DMA, so no register holds them across the MFMA loop and
+    //      no wait for them lands before it: loaded into registers, the compiler spilled them and
+    //      waited vmcnt(0) -- for the next stage's DMA too -- at every tile's last stage; the flags
+    //      come from the prologue's copy in LDS.  Landed at the next vmcnt(0) + barrier.)
+    const uint32_t s2_lds = (uint32_t)(uintptr_t)(lds_u8_t*)S + kFS2Off + wid * 1024u;
+    auto epi_issue = [&](uint32_t mblk, uint32_t ct) {
+        const uint64_t ev = min<uint64_t>((uint64_t)mblk * kDenseTile + er, (uint64_t)a.n - 1u);  // (rows >= n: unused)
+        glds16(a.seen + ev * a.stride + ct * 4u + 2u * ep, s2_lds);
     };
     // ---- the epilogue of tile (mblk, ct): sInc holds its Inc > 0 words ----
-    auto epilogue = [&](uint32_t mblk, uint32_t ct, const EpiIn& in) {
+    auto epilogue = [&](uint32_t mblk, uint32_t ct) {
         const uint32_t w0 = ct * 4u;
         const uint64_t ev = (uint64_t)mblk * kDenseTile + er;
         const uint32_t wa = w0 + 2u * ep;
-        const uint32_t fa = in.fa, fb = in.fb;
-        const bool need_seen = ev < a.n && (((in.lpa | in.lpb) != 0ull) || ((fa | fb) & WF_CLEAR));
-        ulonglong2 s2 = in.s2;
+        const uint32_t f4 = sCtF[ct];
+        const uint32_t fa = (f4 >> (16u * ep)) & 0xffu, fb = (f4 >> (16u * ep + 8u)) & 0xffu;
+        ulonglong2 s2 = sS2[t];
         DSTAMP(3);
         uint64_t n0 = 0ull, n1 = 0ull;
         if (ev < a.n) {
@@ -786,7 +827,7 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
             const bool swr = (n0 | n1) != 0ull || ((fa | fb) & WF_CLEAR) != 0u;
             if (swr) *reinterpret_cast<ulonglong2*>(a.seen + ev * a.stride + wa) = make_ulonglong2(s2.x | n0, s2.y | n1);
             *reinterpret_cast<ulonglong2*>(a.Fnext + ev * a.stride + wa) = make_ulonglong2(n0, n1);
-            t_srd += need_seen;
+            t_srd += 1u;  // (the seen pair is loaded for every row)
             t_swr += swr;
             t_fwr += 1u;
             if (a.snap) {
@@ -836,24 +877,27 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
     // dealt round-robin -- run while it loads
     uint32_t buf = 0;
     uint32_t LM = 0, LC = 0, LS = 0;
-    uint64_t LF = 0;
+    uint64_t LF = 0, LK = 0;  // LK: the current tile's stage mask (one_word)
     uint32_t rk = 0;
     uint64_t rb = 0, re = 0;
     bool have = range_of(0u, rb, re);
     if (have) {
         locate(rb, LM, LC, LS, LF);
+        if (one_word) LK = fused_stages(a, LC, 0u);
         fused_issue(a, S, 0u, LM, LC, LS, wid, lane);
     }
     DSTAMP(0);
     for (uint32_t T = ord; T < a.total; T += G) {
         const uint32_t ct = T % a.nt, mblk = T / a.nt;
         if (!active(ct) || sCtU[ct] != 0u) continue;
-        const EpiIn in = epi_load(mblk, ct);
+        epi_issue(mblk, ct);
         sInc[er * 4u + 2u * ep] = 0ull;
         sInc[er * 4u + 2u * ep + 1u] = 0ull;
-        epilogue(mblk, ct, in);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        epilogue(mblk, ct);
     }
-    DSTAMP(7);
+    DSTAMP(0);  // (epilogue-only tiles: with the prologue)
     // ---- this block's ranges, each a run of units [rb, re); the unit loads chain across them ----
     uint64_t u = rb;
     // A whole tile's epilogue is deferred to just after the next unit's barrier and before that
@@ -862,7 +906,6 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
     // every tile boundary for their acks)
     bool pend = false;
     uint32_t pM = 0, pC = 0;
-    EpiIn pin{};
     while (have) {
         // one tile segment: units [u, end) of tile (mblk, ct) -- the whole tile or a part of it
         const uint32_t mblk = LM, ct = LC;
@@ -878,7 +921,6 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int j = 0; j < 2; j++) acc[i][j] = v16i_t{0};
-        EpiIn ein{};
         // after the segment: the next range when this one ends with it
         bool next_have = true;
         uint32_t next_k = rk;
@@ -888,11 +930,11 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
             // the next unit: the tile's next stage, else the range's next column tile with units,
             // else the first unit of the block's next range
             uint32_t nM = LM, nC = LC, nS = a.nst;
-            uint64_t nF = LF;
+            uint64_t nF = LF, nK = LK;
             bool more = true;
             if (u + 1u < re) {
                 if (u + 1u < tlast) {
-                    nS = stage_from(LC, s + 1u);
+                    nS = one_word ? stage_in(LK, s + 1u) : stage_from(LC, s + 1u);
                 } else {  // the next tile in tile order (one exists: u + 1 < re <= U)
                     const uint32_t g = LM / GM;
                     if (LM - g * GM + 1u < grows(g)) {
@@ -907,7 +949,12 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
                         }
                     }
                     nF = tlast;
-                    nS = stage_from(nC, 0u);
+                    if (!one_word) {
+                        nS = stage_from(nC, 0u);
+                    } else {
+                        if (nC != LC) nK = fused_stages(a, nC, 0u);  // (masks are per column tile)
+                        nS = stage_in(nK, 0u);
+                    }
                 }
             } else {
                 more = false;
@@ -919,6 +966,7 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
                         next_b = b;
                         next_e = e;
                         locate(b, nM, nC, nS, nF);
+                        if (one_word) nK = fused_stages(a, nC, 0u);
                         break;
                     }
                 }
@@ -926,14 +974,15 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
             }
             DSTAMP(2);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            DSTAMP(7);  // (this wave's stage wait)
             __syncthreads();  // stage s landed for every wave; buffer buf ^ 1 is free
             DSTAMP(1);
             if (pend) {  // (no stage in flight: the epilogue's barriers drain nothing)
-                epilogue(pM, pC, pin);
+                epilogue(pM, pC);
                 pend = false;
             }
             if (more) fused_issue(a, S, buf ^ 1u, nM, nC, nS, wid, lane);
-            if (u + 1u == end && whole) ein = epi_load(mblk, ct);  // the epilogue's inputs, early
+            if (u + 1u == end && whole) epi_issue(mblk, ct);  // the epilogue's seen pairs, early
             const uint8_t* As = S + buf * kFStageBytes;
             const uint8_t* Bs = As + kDenseTile * 128u;
 #pragma unroll
@@ -969,30 +1018,15 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
             macs++;
             DSTAMP(2);
             buf ^= 1u;
-            LM = nM; LC = nC; LS = nS; LF = nF;
+            LM = nM; LC = nC; LS = nS; LF = nF; LK = nK;
         }
         // ---- Inc > 0 -> one 64-bit word per (row, word): wave ballots; lane l collects rows l (lo)
         //      and l + 64 (hi) of the wave's 128 (a ballot of register g of MFMA tile (i, j) holds
         //      columns 32j..32j+31 of row (g & 3) + 8 (g >> 2) in its low half, of the row 4 below in
         //      its high half) ----
-        uint64_t lo = 0ull, hi = 0ull;
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int g = 0; g < 16; g++) {
-                const unsigned long long q0 = __ballot(acc[i][0][g] > 0);
-                const unsigned long long q1 = __ballot(acc[i][1][g] > 0);
-                const uint64_t h0 = (q0 & 0xffffffffull) | (q1 << 32);
-                const uint64_t h1 = (q0 >> 32) | (q1 & 0xffffffff00000000ull);
-                const uint32_t row = (uint32_t)(i & 1) * 32u + (g & 3) + 8u * (g >> 2);
-                if (i < 2) {
-                    if (lane == row) lo = h0;
-                    if (lane == row + 4u) lo = h1;
-                } else {
-                    if (lane == row) hi = h0;
-                    if (lane == row + 4u) hi = h1;
-                }
-            }
+        uint32_t rw[4] = {0u, 0u, 0u, 0u};
+        fused_row_words<0>(acc, rw);
+        const uint64_t lo = (uint64_t)rw[0] | ((uint64_t)rw[1] << 32), hi = (uint64_t)rw[2] | ((uint64_t)rw[3] << 32);
         DSTAMP(3);
         const uint64_t vlo = (uint64_t)mblk * kDenseTile + wm * 128u + lane;
         if (whole) {
@@ -1001,7 +1035,6 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
             pend = true;  // (the next unit's barrier orders these writes before the epilogue)
             pM = mblk;
             pC = ct;
-            pin = ein;
         } else {
             // a split tile: OR the partial words into inc, count the units into the tile's ticket;
             // the block completing it takes the words back and runs the epilogue
@@ -1029,9 +1062,10 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
                     sInc[er * 4u + 2u * ep] = 0ull;
                     sInc[er * 4u + 2u * ep + 1u] = 0ull;
                 }
-                const EpiIn in = epi_load(mblk, ct);
+                epi_issue(mblk, ct);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
-                epilogue(mblk, ct, in);
+                epilogue(mblk, ct);
             }
         }
         if (u == re) {  // the range is done: on to the next one (its first unit is already loading)
@@ -1043,8 +1077,9 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
         }
     }
     if (pend) {  // the last tile's epilogue
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        epilogue(pM, pC, pin);
+        epilogue(pM, pC);
     }
     if (a.snap) {
         snap_local = wave_sum(snap_local);

@@ -137,21 +137,28 @@ struct PullArgs {
 // Phase-ordered update of id groups inside one word (rare: only words holding groups).
 // Groups are contiguous bit ranges in phase order; a node's first contact with the id is
 // the lowest-phase arrival, and nothing arrives once any member bit is already seen.
+// The id group holding bit b of gm (groups: contiguous runs of gm, each starting at a bit of gs)
+__device__ __forceinline__ uint64_t group_of(uint32_t b, uint64_t gm, uint64_t gs) {
+    const uint64_t below = gs & (b == 63u ? ~0ull : ((2ull << b) - 1ull));  // starts at or below b
+    const uint32_t s = 63u - (uint32_t)__builtin_clzll(below);
+    const uint64_t above = gs & (s == 63u ? 0ull : ~((2ull << s) - 1ull));  // starts after s
+    const uint64_t upto = above ? ((above & (~above + 1ull)) - 1ull) : ~0ull;
+    return gm & upto & ~((1ull << s) - 1ull);
+}
+// Only the groups holding an incoming bit can change `nw` (a group with none keeps none, seen or
+// not), so the loop visits those -- not every group of the word
 __device__ __forceinline__ uint64_t group_fix(uint64_t nw, uint64_t seen, uint64_t gm,
                                               uint64_t gs) {
-    uint64_t rem = gm;
-    while (rem) {
-        const int s = __ffsll((long long)rem) - 1;
-        const uint64_t above = gs & ~((2ull << s) - 1ull);
-        const uint64_t upto = above ? ((above & (~above + 1ull)) - 1ull) : ~0ull;
-        const uint64_t grp = rem & upto;
+    uint64_t todo = nw & gm;
+    while (todo) {
+        const uint64_t grp = group_of((uint32_t)__builtin_ctzll(todo), gm, gs);
         if (seen & grp) {
             nw &= ~grp;
         } else {
             const uint64_t x = nw & grp;
             nw = (nw & ~grp) | (x & (~x + 1ull));
         }
-        rem &= ~grp;
+        todo &= ~grp;
     }
     return nw;
 }
@@ -2147,7 +2154,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             e0 = get_event();
             e1 = get_event();
             HIP_TRY(hipEventRecord(e0, stream));
-            if (ny && !dense) {
+            if (!dense) {  // (every tick: a tick without young tiles is a phase of k_pull alone)
                 p0 = get_event();
                 HIP_TRY(hipEventRecord(p0, stream));
             }
@@ -2254,6 +2261,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 if ((rc = end_chunk(c))) return rc;
             }
             if (pts) k_phase_acc<<<1, 1, 0, stream>>>(pts);  // (row chunks: the chunks' births are inside the span)
+            if (p0) event_pool.push_back(p0);  // (timed per chunk above)
         } else if (fused_tick) {
             // the whole DENSE pull in one persistent kernel (contraction, dedup, FT of F_next)
             FusedArgs f;
@@ -2318,6 +2326,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             if (cfg.flags & GOSSIP_F_TIMING) {
                 HIP_TRY(hipEventRecord(e1, stream));
                 timers.emplace_back(e0, e1);
+                if (p0) event_pool.push_back(p0);  // (no phase timer on this path)
             }
         } else {
             if (overlap) {
@@ -2338,7 +2347,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 const int rc = launch_young(stream);
                 if (rc) return rc;
             }
-            if (ny && (cfg.flags & GOSSIP_F_TIMING)) {  // the whole pull phase
+            if (p0 && (cfg.flags & GOSSIP_F_TIMING)) {  // the whole pull phase
                 p1 = get_event();
                 HIP_TRY(hipEventRecord(p1, stream));
                 timers_phase.emplace_back(p0, p1);

@@ -127,14 +127,11 @@ __host__ __device__ constexpr size_t young_lds_bytes(uint32_t ny, uint32_t nr) {
 // x with every id group it touches made whole (gm / gs: the word's group bits and group starts;
 // groups are contiguous runs, group_fix's layout)
 __device__ __forceinline__ uint64_t group_expand(uint64_t x, uint64_t gm, uint64_t gs) {
-    uint64_t rem = gm, out = x;
-    while (rem & x) {
-        const int s = __ffsll((long long)rem) - 1;
-        const uint64_t above = gs & ~((2ull << s) - 1ull);
-        const uint64_t upto = above ? ((above & (~above + 1ull)) - 1ull) : ~0ull;
-        const uint64_t grp = rem & upto;
-        if (x & grp) out |= grp;
-        rem &= ~grp;
+    uint64_t todo = x & gm, out = x;  // (the groups holding a bit of x, group_fix)
+    while (todo) {
+        const uint64_t grp = group_of((uint32_t)__builtin_ctzll(todo), gm, gs);
+        out |= grp;
+        todo &= ~grp;
     }
     return out;
 }
@@ -459,13 +456,18 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
                         // (a list holds every bit of a seen group: the accumulator has none of them)
                         x = s_acc[i] & ~sv;
                         if (f & WF_KEEP) x &= a.ctl[w].keep;  // (loaded and used in the branch)
-                        if (f & WF_GROUP) x = group_fix(x, sv, a.ctl[w].gmask, a.ctl[w].gstart);
+                        uint64_t gm = 0ull, gs = 0ull;  // (one load of the group masks: fix and expand)
+                        if (f & WF_GROUP) {
+                            gm = a.ctl[w].gmask;
+                            gs = a.ctl[w].gstart;
+                            x = group_fix(x, sv, gm, gs);
+                        }
                         if constexpr (LO) {
                             if (x) a.seen[v * stride + w] = sv | x;
                         }
                         if (a.snap && (f & WF_SNAP)) snap_local += (unsigned long long)__popcll(x & a.ctl[w].snap);
                         s_acc[i] = x;  // the node's new bits, for the outputs below
-                        if constexpr (!LO) xe = (f & WF_GROUP) ? group_expand(x, a.ctl[w].gmask, a.ctl[w].gstart) : x;
+                        if constexpr (!LO) xe = (f & WF_GROUP) ? group_expand(x, gm, gs) : x;
                     }
                     cnt += (uint32_t)__popcll(x);
                     if constexpr (LO) {
