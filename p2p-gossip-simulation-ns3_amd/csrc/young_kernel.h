@@ -411,7 +411,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             }
             // kept entries -> s_lst[1, kept]
             uint32_t kept = 0;
-            {
+            YDUP(10) {
                 const uint32_t c = (uint32_t)__builtin_popcount(keepm);
                 const uint32_t incl = wave_incl_scan(c);
                 uint32_t pos = 1u + incl - c;
@@ -456,18 +456,13 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
                         // (a list holds every bit of a seen group: the accumulator has none of them)
                         x = s_acc[i] & ~sv;
                         if (f & WF_KEEP) x &= a.ctl[w].keep;  // (loaded and used in the branch)
-                        uint64_t gm = 0ull, gs = 0ull;  // (one load of the group masks: fix and expand)
-                        if (f & WF_GROUP) {
-                            gm = a.ctl[w].gmask;
-                            gs = a.ctl[w].gstart;
-                            x = group_fix(x, sv, gm, gs);
-                        }
+                        if (f & WF_GROUP) x = group_fix(x, sv, a.ctl[w].gmask, a.ctl[w].gstart);
                         if constexpr (LO) {
                             if (x) a.seen[v * stride + w] = sv | x;
                         }
                         if (a.snap && (f & WF_SNAP)) snap_local += (unsigned long long)__popcll(x & a.ctl[w].snap);
                         s_acc[i] = x;  // the node's new bits, for the outputs below
-                        if constexpr (!LO) xe = (f & WF_GROUP) ? group_expand(x, gm, gs) : x;
+                        if constexpr (!LO) xe = (f & WF_GROUP) ? group_expand(x, a.ctl[w].gmask, a.ctl[w].gstart) : x;
                     }
                     cnt += (uint32_t)__popcll(x);
                     if constexpr (LO) {
@@ -613,7 +608,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
                 }
             }
             // ---- the new seen list: whole lines; an overflow marks the header ----
-            if (!lovf) {
+            YDUP(9) if (!lovf) {
                 if (lane == 0) s_lst[0] = (uint16_t)(lspill ? kListOverflow : list_header(kept, lcount));
                 __builtin_amdgcn_wave_barrier();
                 const uint32_t lines = (!lspill && lcount > 63u) ? 2u : 1u;
@@ -623,7 +618,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
                 t_lw += lines;
             }
             // ---- reset the touched accumulator words, counters ----
-            for (uint32_t t = lane; t < ntouch; t += 64) s_acc[s_list[t]] = 0ull;
+            YDUP(9) for (uint32_t t = lane; t < ntouch; t += 64) s_acc[s_list[t]] = 0ull;
             __builtin_amdgcn_wave_barrier();
             // fresh write-sparse tiles [nr, ny) of a node whose list overflowed (earlier): clear
             // their dense seen words (stale from the tiles' previous use; k_births sets this tick's
