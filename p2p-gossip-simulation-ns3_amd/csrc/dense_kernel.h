@@ -429,6 +429,7 @@ struct FusedArgs {
     uint32_t* tix;                         // per tile: units reduced so far (zero between uses)
     uint32_t rmax;                         // most data-parallel rounds (A/B: GOSSIP_DENSE_ROUNDS)
     uint32_t gm;                           // row blocks per tile group (tile order, header comment)
+    unsigned long long* pts;               // nullable: [4] block 0's start, [5] max block end (phase timer)
 };
 
 constexpr uint32_t kFStageBytes = 2u * kDenseTile * 128u;  // A + B rows of one 1024-k stage
@@ -608,6 +609,7 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
     const ulonglong2* sS2 = reinterpret_cast<const ulonglong2*>(S + kFS2Off);  // thread t's seen pair
     const uint32_t t = threadIdx.x, lane = t & 63u, wid = wave_in_block();
     const uint32_t wm = wid >> 2, wn = wid & 3u;
+    if (a.pts && blockIdx.x == 0 && t == 0) a.pts[4] = __builtin_amdgcn_s_memrealtime();  // (dispatched first)
     for (uint32_t i = blockIdx.x * 512u + t; i < a.snz_zwords; i += gridDim.x * 512u) a.snz_z[i] = 0ull;
     // Per column tile ct (thread t, +512): its 4 flag bytes, its 4 live_prev words and its stage
     // masks, all loaded before any is used (one round trip).  Active 16-word tiles (header comment:
@@ -1084,6 +1086,10 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
     if (a.snap) {
         snap_local = wave_sum(snap_local);
         if (lane == 0 && snap_local) atomicAdd(a.snap, snap_local);
+    }
+    if (a.pts) {  // (every wave's last store issued; the end stamp of the block's last wave)
+        __syncthreads();
+        if (t == 0) atomicMax(&a.pts[5], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
 #ifdef DENSE_STAMPS
     if (a.acct && lane == 0)

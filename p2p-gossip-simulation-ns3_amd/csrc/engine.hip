@@ -557,10 +557,20 @@ __global__ __launch_bounds__(256) void k_sum_u32(const uint32_t* a, const uint32
 // k_phase_start runs when the kernel before the phase has finished, k_phase_acc when the phase's
 // last kernel has, and adds the span to ts[2] (ts[3] counts them).  Round 4 stamped from every
 // block of the phase kernels with same-address atomics, which slowed k_transpose 6x.
-__global__ void k_phase_start(unsigned long long* ts) { ts[0] = __builtin_amdgcn_s_memrealtime(); }
+// A fused tick whose kernel stamps itself (ts[4] = block 0's start, ts[5] = the last block's end:
+// one no-return atomicMax per block as it ends) takes that span: the two stamp kernels' launch
+// gaps (~6 us each on C2) are not the phase's.
+__global__ void k_phase_start(unsigned long long* ts) {
+    ts[0] = __builtin_amdgcn_s_memrealtime();
+    ts[4] = ~0ull;
+    ts[5] = 0ull;
+}
 __global__ void k_phase_acc(unsigned long long* ts) {
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-    if (now > ts[0]) ts[2] += now - ts[0];
+    if (ts[5] > ts[4])
+        ts[2] += ts[5] - ts[4];
+    else if (now > ts[0])
+        ts[2] += now - ts[0];
     ts[3] += 1ull;
 }
 
@@ -709,7 +719,7 @@ struct gossip_engine {
     unsigned long long* d_inc = nullptr;  // n x stride incoming words (GEMM -> pull)
     uint32_t *d_recv = nullptr, *d_gen = nullptr, *d_effgen = nullptr;
     uint64_t* d_sent = nullptr;
-    unsigned long long* d_phase_ts = nullptr;  // DENSE phase span: [0] start (min), [1] end (max), [2] sum of spans
+    unsigned long long* d_phase_ts = nullptr;  // DENSE phase span: [0] start, [2] sum of spans, [3] count, [4]/[5] fused kernel's own start / end
     unsigned long long* d_live[3] = {nullptr, nullptr, nullptr};  // liveness ring (tick % 3)
     unsigned long long* d_scalars = nullptr;  // [0]=scratch, [1..]=snapshot base/partial
     unsigned long long* d_acct = nullptr;     // k_pull traffic accounting (since reset)
@@ -1242,7 +1252,7 @@ int gossip_engine::alloc_device() {
     HIP_TRY(hipMalloc(&d_effgen, (size_t)n * 4));
     HIP_TRY(hipMalloc(&d_sent, (size_t)n * 8));
     {
-        const unsigned long long init[4] = {~0ull, 0ull, 0ull, 0ull};
+        const unsigned long long init[6] = {~0ull, 0ull, 0ull, 0ull, ~0ull, 0ull};
         HIP_TRY(hipMalloc(&d_phase_ts, sizeof(init)));
         HIP_TRY(hipMemcpy(d_phase_ts, init, sizeof(init), hipMemcpyHostToDevice));
     }
@@ -2280,6 +2290,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             f.inc = d_inc;
             f.tix = d_tix;
             f.rmax = dense_rounds < 0 ? 0xffffffffu : (uint32_t)dense_rounds;
+            f.pts = (pts && ft_valid) ? pts : nullptr;  // (a tick with k_transpose keeps the stamp-kernel span)
             f.gm = (uint32_t)std::min<int64_t>(dense_gm, 64);
             uint32_t fg = (uint32_t)std::min<uint64_t>(f.total, (uint64_t)num_cus);
             if (fg >= 8u) fg &= ~7u;

@@ -57,9 +57,11 @@ def _burst(gossip):
 
 
 def _budget(gossip, ev):
-    """A device-memory budget between what 2 shards and what 1 engine hold for the burst, from the
-    engines' own reported need (gossip_counters.device_bytes after an unconstrained run) -- not a
-    constant, so the test follows any change of the engine's layout."""
+    """A device-memory budget that one engine cannot meet for the burst and each of 2 shards can,
+    from the engines' own reported need (gossip_counters.device_bytes) -- not a constant, so the
+    test follows any change of the engine's layout: below what one engine holds with exactly the
+    window the run reached (it cannot shrink further), above what a 2-shard engine allocates on
+    its own (its window estimate and headroom included: the fallback run allocates that)."""
     topo = gossip.Topology.gnp(N_BURST, 16.0 / (N_BURST - 1), 8, gossip.TOPO_SKIP)
     t_cut = gossip.seconds_to_ns(5.2)
 
@@ -73,19 +75,9 @@ def _budget(gossip, ev):
         eng.close()
         return c
 
-    def need(shards):
-        # the window the run reached (an unconstrained engine also allocates headroom), then the
-        # bytes an engine holds with exactly that window
-        out = 0
-        for r in range(shards):
-            hw = run(shards, r).words_hw
-            c = run(shards, r, max_words=hw)
-            out = max(out, c.device_bytes)
-        return out
-
-    one, two = need(1), need(2)
-    assert two < one, (one, two)
-    mib = (one + two) // 2 >> 20  # (the CLI takes whole MB)
+    one = run(1, 0, max_words=run(1, 0).words_hw).device_bytes  # (exactly the reached window)
+    two = max(run(2, r).device_bytes for r in range(2))           # (as allocated unconstrained)
+    mib = (one >> 20) - 1  # (the CLI takes whole MB)
     assert two < mib << 20 < one, (one, two, mib)
     return mib
 

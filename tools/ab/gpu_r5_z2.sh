@@ -1,0 +1,17 @@
+# Round 5 final evidence, part 2: the driver's C4 command with its CPU baseline, the rocprofv3
+# kernel trace + stats of the same command, and its two PMC passes (FETCH_SIZE, WRITE_SIZE) ->
+# profiles/pmc_C4*.json keyed by this build (tools/pmc_traffic.py --bench-json).
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out
+cd $R
+timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r5z2_bench.json 2> gpurun_out/r5z2_bench.err || { tail -5 gpurun_out/r5z2_bench.err; exit 1; }
+python tools/ab_line.py final gpurun_out/r5z2_bench.json
+cd /tmp && export TMPDIR=/tmp
+B="python $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline"
+timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r5z2_trace -o run --output-format csv -- $B > $R/gpurun_out/r5z2_trace.json 2> $R/gpurun_out/r5z2_trace.err || { echo "trace failed"; tail -3 $R/gpurun_out/r5z2_trace.err; exit 1; }
+echo trace ok
+timeout -s KILL 450 rocprofv3 --kernel-include-regex "k_pull" --pmc FETCH_SIZE -d $R/gpurun_out/r5z2_pmcF -o run --output-format csv -- $B > $R/gpurun_out/r5z2_pmcF.json 2> $R/gpurun_out/r5z2_pmcF.err || { echo "pmcF failed"; tail -3 $R/gpurun_out/r5z2_pmcF.err; exit 1; }
+echo pmcF ok
+timeout -s KILL 450 rocprofv3 --kernel-include-regex "k_pull" --pmc WRITE_SIZE -d $R/gpurun_out/r5z2_pmcW -o run --output-format csv -- $B > $R/gpurun_out/r5z2_pmcW.json 2> $R/gpurun_out/r5z2_pmcW.err || { echo "pmcW failed"; tail -3 $R/gpurun_out/r5z2_pmcW.err; exit 1; }
+echo pmcW ok
