@@ -59,25 +59,27 @@ def _burst(gossip):
 def _budget(gossip, ev):
     """A device-memory budget that one engine cannot meet for the burst and each of 2 shards can,
     from the engines' own reported need (gossip_counters.device_bytes) -- not a constant, so the
-    test follows any change of the engine's layout: below what one engine holds with exactly the
-    window the run reached (it cannot shrink further), above what a 2-shard engine allocates on
-    its own (its window estimate and headroom included: the fallback run allocates that)."""
+    test follows any change of the engine's layout.  Under a budget an engine allocates its window
+    estimate without the headroom an unbudgeted one adds (engine.hip) and fails with
+    GOSSIP_ECAPACITY when that does not fit, so the budget lies between what 2 shards and what 1
+    engine allocate under a budget."""
     topo = gossip.Topology.gnp(N_BURST, 16.0 / (N_BURST - 1), 8, gossip.TOPO_SKIP)
     t_cut = gossip.seconds_to_ns(5.2)
 
-    def run(shards, r, max_words=0):
-        eng = gossip.Engine(N_BURST, 5_000_000, T0, t_cut, shard_rank=r, shard_count=shards, max_words=max_words)
+    def need(shards, r):
+        eng = gossip.Engine(N_BURST, 5_000_000, T0, t_cut, shard_rank=r, shard_count=shards)
+        eng.set_option("mem_limit", 1 << 30)  # (a budget: no headroom)
         eng.set_topology(topo)
         eng.set_schedule(ev)
         eng.run()
         eng.sync()
         c = eng.counters()
         eng.close()
-        return c
+        return c.device_bytes
 
-    one = run(1, 0, max_words=run(1, 0).words_hw).device_bytes  # (exactly the reached window)
-    two = max(run(2, r).device_bytes for r in range(2))           # (as allocated unconstrained)
-    mib = (one >> 20) - 1  # (the CLI takes whole MB)
+    one = need(1, 0)
+    two = max(need(2, r) for r in range(2))
+    mib = (one + two) // 2 >> 20  # (the CLI takes whole MB)
     assert two < mib << 20 < one, (one, two, mib)
     return mib
 
