@@ -245,6 +245,19 @@ constexpr int kWideLanes = 32;
 
 template <int LPW, int EPN>
 void launch_pull_t(bool nt, uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
+    if constexpr (LPW == 32 && EPN == 1) {
+        // the flags k_pull<.., SP = true> takes as compile-time constants (pull_kernel.h): the
+        // same conditions the kernel derives at run time
+        const bool sp = a.tmask != nullptr && a.ptile != nullptr && a.sat != nullptr &&
+                        a.nptile / (uint32_t)(LPW / 8) <= kPullMaxPasses && !a.noskip && a.gate_seen;
+        if (sp) {
+            if (nt)
+                k_pull<LPW, 1, true, true><<<grid, 256, lds, s>>>(a);
+            else
+                k_pull<LPW, 1, false, true><<<grid, 256, lds, s>>>(a);
+            return;
+        }
+    }
     if constexpr ((LPW == 64 || LPW == 32 || LPW == 16) && EPN == 1) {
         if (nt) {
             k_pull<LPW, 1, true><<<grid, 256, lds, s>>>(a);

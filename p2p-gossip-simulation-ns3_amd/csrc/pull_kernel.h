@@ -168,8 +168,13 @@ __device__ __forceinline__ uint32_t pull_cid_load(const PullArgs& a, uint32_t st
     return (c0 + idx < a.n && jj < end) ? (uint32_t)a.col[jj] : 0xffffffffu;
 }
 
-template <int LPW, int EPN, bool NT = false>
-__global__ __launch_bounds__(256) void k_pull(PullArgs a) {
+// SP (the C4 launch, engine.hip launch_pull_t): tile lists with dense-row tiles, saturation bits,
+// empty-item skipping and the own-seen gate all on and no diagnostic no-skip -- compile-time
+// flags instead of runtime ones (each runtime flag held a 64-bit SGPR mask; the kernel spilled
+// SGPRs into VGPR lanes, and every reload in the item loop is a VALU instruction)
+template <int LPW, int EPN, bool NT = false, bool SP = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP ? 5 : 1))) void k_pull(PullArgs a) {
+    const bool noskip = SP ? false : a.noskip != 0u;
     constexpr int GRP = LPW * EPN;  // lanes per node
     constexpr int NPW = 64 / GRP;   // nodes per wave step
     static_assert(GRP <= 64 && (64 % GRP) == 0, "lane layout");
@@ -182,15 +187,15 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
     for (uint32_t i = threadIdx.x; i < a.wact; i += 256) {
         const uint8_t f = a.wflags[a.wbase + i];
         // a young word is k_pull_young's: dead here, no clear, no write
-        s_lp[i] = (f & WF_YOUNG) ? 0ull : (a.live_prev && !a.noskip) ? a.live_prev[a.wbase + i] : ~0ull;
+        s_lp[i] = (f & WF_YOUNG) ? 0ull : (a.live_prev && !noskip) ? a.live_prev[a.wbase + i] : ~0ull;
         s_new[i] = 0ull;
         s_wf[i] = (f & WF_YOUNG) ? (uint8_t)0 : f;
         if (a.keep_lds) s_keep[i] = (f & WF_KEEP) ? a.ctl[a.wbase + i].keep : ~0ull;
     }
     for (uint32_t i = threadIdx.x; i < a.nptile; i += 256) s_pt[i] = a.ptile[i];
     // saturation bits and dense-row tiles (the gathering pull over tile lists only)
-    const bool tm_on = EPN == 1 && a.tmask != nullptr && a.ptile != nullptr;  // dense rows (+ sat)
-    const bool sat_on = tm_on && a.sat != nullptr;
+    const bool tm_on = SP || (EPN == 1 && a.tmask != nullptr && a.ptile != nullptr);  // dense rows (+ sat)
+    const bool sat_on = SP || (tm_on && a.sat != nullptr);
     unsigned long long* s_tm = reinterpret_cast<unsigned long long*>(
         reinterpret_cast<char*>(smem) + pull_lds_bytes(a.wact, a.keep_lds != 0, a.nptile));
     unsigned long long* s_sat = s_tm + 8;  // [wave][node of the chunk][occupancy word of the launch]
@@ -207,7 +212,7 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
     // (WF_CLEAR, WF_DW, WF_KEEP) and the last pass of each occupancy word (the node's nz and sat
     // words are written back there, its counters after the last pass) are never skipped.
     constexpr uint32_t TPP_ = LPW >= 8 ? (uint32_t)LPW / 8u : 1u;
-    const bool skip_on = tm_on && a.nptile / TPP_ <= kPullMaxPasses;
+    const bool skip_on = SP || (tm_on && a.nptile / TPP_ <= kPullMaxPasses);
     __syncthreads();  // (s_lp, s_wf, s_pt written)
     if (skip_on && threadIdx.x < 64u) {
         const uint32_t p = threadIdx.x, np = a.nptile / TPP_;
@@ -247,7 +252,7 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
     // Pass geometry: consecutive 2 LPW-word passes, or (pull_tiles) LPW / 8 listed tiles per pass
     constexpr uint32_t TPP = LPW >= 8 ? (uint32_t)LPW / 8u : 1u;
-    const bool listed = a.ptile != nullptr;
+    const bool listed = SP || a.ptile != nullptr;
     const uint32_t npass = listed ? a.nptile / TPP : (a.wact + 2u * LPW - 1u) / (2u * LPW);
     // launch-local word of this lane's pair in pass p (kNoWord: none)
     auto lw_of = [&](uint32_t p, uint32_t wl) -> uint32_t {
@@ -367,7 +372,7 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
         unsigned long long nzor = 0ull;
         bool nz_new = true, s2c_gated = false;
         int32_t beg = 0, end = 0;  // the current node's peer range (read once per node)
-        const bool gate = gather && !a.noskip && a.gate_seen;
+        const bool gate = gather && (SP || (!noskip && a.gate_seen));
         // the first item's loads have landed before the item loop: inside it, every load is
         // then waited for by the item that issued it or the next (a loop header that merged a
         // pending first-item load would make every item wait for its own prefetches)
@@ -470,7 +475,7 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
             // masked out of `new`, so new = incoming & want (and peers beyond covering `want`
             // add nothing).  Only `want` is carried past the gather.
             const uint64_t want0 = lp0 & ~s2.x & k0, want1 = lp1 & ~s2.y & k1;
-            const bool need = act && !dead && !s2c_gated && (a.noskip || (want0 | want1) != 0ull);
+            const bool need = act && !dead && !s2c_gated && (noskip || (want0 | want1) != 0ull);
             // Columns are allocated in 16-word tiles (one 128-B line per row, engine.hip), so the
             // read decision is made per tile: the 8 word-lanes of a tile load together and every
             // fetched line is fully used.
@@ -496,7 +501,7 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
                         // (a dense-row tile: every peer's row, whatever its occupancy word says)
                         const uint32_t nzp = pass_bits(nzw | drm, pass);
                         for (int t0 = 0; t0 < rem; t0 += kInflight) {
-                            int open = (a.noskip || !late)
+                            int open = (noskip || !late)
                                            ? 1 : (((want0 & ~acc0) | (want1 & ~acc1)) != 0ull);
                             open = (int)group_or<8>((uint32_t)open, lane);  // per tile (8 word-lanes)
                             int gopen = open;
@@ -594,7 +599,7 @@ __global__ __launch_bounds__(256) void k_pull(PullArgs a) {
             // tile occupancy of F_next: the 8 word-lanes of a tile agree on writing the row
             // (NOSKIP diagnostic: every tile row is written and marked occupied, so the pull
             // reads every peer row -- the dense-pull byte count)
-            int ta = (n0 | n1) != 0ull || (a.noskip && act);
+            int ta = (n0 | n1) != 0ull || (noskip && act);
             ta = (int)group_or<8>((uint32_t)ta, lane);
             // a WF_DW tile's row is written at every node (zeros too): read as a dense row next tick
             const bool trow = ta || (act && (f0 & WF_DW));
