@@ -1,5 +1,6 @@
 # Round 5: one rank of the 8-GPU C4 layout under the birth-tick rule (bench's auto rule at 8 shards),
-# young tiles auto / off / young_age 3 / 4 -- engine options by environment, same box.
+# young tiles auto / off / young_age 3 / 4 (first call), auto / young_age 6 / 7 (second) -- engine
+# options by environment, same box.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
@@ -10,6 +11,8 @@ run() {  # name, env...
   python tools/ab_line.py $name gpurun_out/r5q_$name.json
 }
 run auto X=1
-run young0 GOSSIP_YOUNG=0
-run age3 GOSSIP_YOUNG_AGE=3
-run age4 GOSSIP_YOUNG_AGE=4
+run age6 GOSSIP_YOUNG_AGE=6
+run age7 GOSSIP_YOUNG_AGE=7
+
+
+
