@@ -298,6 +298,13 @@ def rehearse_rows(args, wl, topo, ev, shards, R, flags):
     print(json.dumps(out), flush=True)
 
 
+def resolve_shard_rule(rule, shards):
+    """--shard-rule auto: the birth-tick rule from 8 share shards on, the hash rule below (one-rank
+    rehearsals, DESIGN.md section 5: 8 shards 24.8 vs 27.6 ms per tick; 4 shards 39.8 vs 36.7;
+    2 shards: the tick rule's window peaks overflow the capacity estimate)."""
+    return rule if rule != "auto" else ("tick" if shards >= 8 else "hash")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -365,7 +372,7 @@ def main():
     flags = gossip.F_TIMING | (gossip.F_NOSKIP if args.noskip else 0)
 
     def shard_rule(shards):
-        return args.shard_rule if args.shard_rule != "auto" else ("tick" if shards >= 8 else "hash")
+        return resolve_shard_rule(args.shard_rule, shards)
     if rank == 0:
         rp, _, _ = topo.csr()
         log(f"[bench] {wl['desc']}: {topo.num_nodes} nodes, {int(rp[-1])} directed entries, "

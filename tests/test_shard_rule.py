@@ -4,6 +4,8 @@ Shares are independent floods except inside an id instance -- the generations th
 within one connected component share one seen-set entry (p2pnode.cc:189) -- so a rule may split
 the instances over shards any way it likes as long as every instance stays whole.  The birth-tick
 rule (GOSSIP_F_SHARD_BY_TICK) gives an instance to shard (tick of its first generation) mod S."""
+import os
+
 import numpy as np
 from scipy.sparse import csr_matrix
 from scipy.sparse.csgraph import connected_components
@@ -56,3 +58,15 @@ def test_birth_tick_rule_fills_a_shard_per_tick(gossip):
     for t in np.unique(tick):
         assert len(np.unique(owner[tick == t])) == 1
     assert np.array_equal(np.bincount(owner, minlength=4) > 0, [True] * 4)
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_auto_rule_takes_birth_ticks_from_8_shards():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert [bench.resolve_shard_rule("auto", s) for s in (1, 2, 4, 8, 16)] == ["hash", "hash", "hash", "tick", "tick"]
+    assert bench.resolve_shard_rule("hash", 8) == "hash" and bench.resolve_shard_rule("tick", 2) == "tick"
