@@ -52,7 +52,7 @@ def main():
     variants = [("default", ())]
     if a.variants:
         variants += [("late_age 0", (("late_age", 0),)), ("pull_gate 0", (("pull_gate", 0),)),
-                     ("late 0 + gate 0 + lpw 64", (("late_age", 0), ("pull_gate", 0), ("pull_lpw", 64)))]
+                     ("late 0 + gate 0", (("late_age", 0), ("pull_gate", 0)))]
     ref = None
     for name, opts in variants:
         dc, cc = deltas(topo, ev, t0, t1, opts)
