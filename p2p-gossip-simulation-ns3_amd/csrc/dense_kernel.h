@@ -369,18 +369,19 @@ __global__ __launch_bounds__(1024) void k_dense_dedup(PullArgs a) {
 // Work: tiles of 256 rows x 256 columns; per tile only the K stages whose frontier bits are
 // non-zero are computed: the producer of FT (this kernel's epilogue at t-1, plus k_births, or
 // k_transpose) sets a per-(column tile, stage) bit, so an empty stage is neither loaded nor
-// multiplied.  A (tile, non-empty stage) pair is a UNIT.  Schedule: one block per CU; the live
-// tiles (tile order, row block major) go out in data-parallel ROUNDS, block b taking tile r G + b
-// in round r (the blocks of one XCD take adjacent tiles: the column tiles of one row block, whose
-// adjacency rows then stay in that XCD's L2), and the last partial round -- the tail, fewer tiles
-// than blocks -- is split stream-K: its units are cut into G equal contiguous ranges, so no CU
-// waits for a whole tile while others idle (C2: ~600 live tiles of 4 stages on 256 CUs).  A tile
-// split between blocks is reduced by OR: Inc > 0 iff some partial sum is > 0 (all products are
-// >= 0), so each block ORs its partial row words into `inc` (atomics), counts its units into the
-// tile's ticket, and the block that completes the ticket takes the words back (atomic exchange
-// with 0) and runs the epilogue.  (Pure stream-K over all units -- one contiguous range per block
-// -- measured slower on C5: each block then streams adjacency rows no other block of its XCD is
-// reading, 11.0 / 9.98 ms per full tick against 9.36 / 8.99 ms in rounds.)  Stages arrive by LDS-DMA (global_load_lds_dwordx4,
+// multiplied.  A (tile, non-empty stage) pair is a UNIT.  Schedule: one block per CU (XCD-major
+// block order); the live tiles, in GROUPED order (groups of GM row blocks, column tile major
+// within a group, so the blocks of one XCD share a few adjacency row blocks and FT tiles in its
+// L2), go out in at most `rmax` data-parallel ROUNDS, block b taking tile r G + b in round r.  The
+// remaining tiles are the tail: their units, in the same order, fill each block's DEFICIT below
+// the mean load ceil(U / G) (column tiles differ in non-empty stages, so the rounds leave blocks
+// unevenly loaded), so no CU waits for a whole tile while others idle.  A tile split between
+// blocks is reduced by OR: Inc > 0 iff some partial sum is > 0 (all products are >= 0), so each
+// block ORs its partial row words into `inc` (atomics), counts its units into the tile's ticket,
+// and the block that completes the ticket takes the words back (atomic exchange with 0) and runs
+// the epilogue.  (Pure stream-K over all units -- one equal contiguous range per block --
+// measured slower on C5: a block's range spans row blocks no other block of its XCD is reading;
+// DESIGN.md §3.)  Stages arrive by LDS-DMA (global_load_lds_dwordx4,
 // 16 B per lane, no VGPR staging) into two 64-KB buffers; the next (tile, stage) is issued as soon
 // as the current one has landed -- across tile boundaries, so the next tile's first stage loads
 // while this tile's epilogue runs.  The LDS image is lane-linear per 1-KiB DMA piece (8 rows of
