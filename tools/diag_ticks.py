@@ -1,47 +1,61 @@
 #!/usr/bin/env python3
-"""Per-tick diagnostics of the engine on the C3 workload (GPU): window width, pull time,
-bytes moved, pair-edge reads, edge events.  Syncs after every tick (diagnostic only).
+"""Diagnostic: per-tick pull counters of one share shard of the C4 bench (bench.py's setup).
 
-    python tools/diag_ticks.py [--ticks 80] [--nodes 1000000]
-"""
+    python tools/diag_ticks.py [--shards 8] [--rule tick|hash] [--ticks 16] [--warmup 5]
+
+Ramps shard 0 of S exactly as bench.py does, then runs the ticks one at a time, resetting the
+device tallies before each (Engine.reset_timing), and prints one JSON line per tick: the pull
+phase and kernel times, k_pull's items / gathering items / peer-row loads / occupancy reads /
+own-seen reads, and k_pull_young's slot lines -- the per-age costs of DESIGN.md §5."""
 import argparse
+import json
 import os
 import sys
-import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "p2p-gossip-simulation-ns3_amd"))
 import gossip  # noqa: E402
+import gossip.workloads as WL  # noqa: E402
+from bench import L_NS, SLICE_NS, T0_NS, T_CUT_NS  # noqa: E402
 
-T0, L, TCUT = 5_000_000_000, 5_000_000, 59_900_000_000
+FIELDS = ("pull_ms", "young_ms", "pull_phase_ms", "pull_launches", "young_launches", "pull_items",
+          "pull_gather_items", "pull_pair_edges", "pull_col_ids", "pull_nz_reads", "pull_seen_reads",
+          "pull_sat_skips", "pull_bytes_moved", "young_slot_lines", "young_bytes_moved")
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ticks", type=int, default=80)
-    ap.add_argument("--nodes", type=int, default=1_000_000)
-    ap.add_argument("--deg", type=float, default=16.0)
-    ap.add_argument("--max-words", type=int, default=0)
+    ap.add_argument("--shards", type=int, default=8)
+    ap.add_argument("--rule", choices=["tick", "hash"], default="tick")
+    ap.add_argument("--ticks", type=int, default=16)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--threads", type=int, default=16)
     a = ap.parse_args()
-    n = a.nodes
-    topo = gossip.Topology.gnp(n, a.deg / (n - 1), 3, gossip.TOPO_SKIP, threads=16)
-    ev = gossip.make_schedule(n, 1000, T0, TCUT, t_gen_end_ns=T0 + (a.ticks + 1) * L, threads=16)
-    eng = gossip.Engine(n, L, T0, TCUT, flags=gossip.F_TIMING, max_words=a.max_words)
-    eng.set_topology(topo)
-    eng.set_schedule(ev)
-    t0 = eng.first_tick
-    prev = eng.counters()
-    print("tick words pull_ms moved_GB pair_edges_M edge_events_G births", flush=True)
-    for k in range(a.ticks):
-        eng.run(t0 + k + 1)
+    n = WL.CONFIGS["C4"]["nodes"]
+    topo = WL.topology("C4", nodes=n, threads=a.threads)
+    ev, _ = WL.slice_schedule(n, WL.CONFIGS["C4"]["node_seed"], SLICE_NS,
+                              SLICE_NS + (a.warmup + a.ticks + 1) * L_NS, threads=a.threads)
+    flags = gossip.F_TIMING | (gossip.F_SHARD_BY_TICK if a.rule == "tick" else 0)
+    eng = gossip.Engine(n, L_NS, T0_NS, T_CUT_NS, flags=flags, shard_rank=0, shard_count=a.shards)
+    try:
+        eng.set_topology(topo)
+        eng.set_schedule(ev)
+        t = SLICE_NS // L_NS + a.warmup
+        eng.run(t)
         eng.sync()
-        c = eng.counters()
-        births = int(((ev["ns"] // L) == t0 + k).sum())
-        print(f"{t0 + k} {c.words_hw} {c.pull_ms - prev.pull_ms:.3f} "
-              f"{(c.pull_bytes_moved - prev.pull_bytes_moved) / 1e9:.2f} "
-              f"{(c.pull_pair_edges - prev.pull_pair_edges) / 1e6:.1f} "
-              f"{(c.edge_events - prev.edge_events) / 1e9:.2f} {births}", flush=True)
-        prev = c
+        for _ in range(a.ticks):
+            e0 = eng.counters().edge_events
+            eng.reset_timing()
+            t += 1
+            eng.run(t)
+            eng.sync()
+            c = eng.counters()
+            row = {"tick": t, "edge_events": c.edge_events - e0}
+            row.update({f: getattr(c, f) for f in FIELDS})
+            print(json.dumps(row), flush=True)
+    finally:
+        eng.close()
 
 
 if __name__ == "__main__":
