@@ -1941,7 +1941,7 @@ int gossip_engine::tick_step_a(int64_t t) {
             };
             uint32_t group_tw = 0xffffffffu;
             for (uint32_t tl = t0; tl < t1; tl++) {
-                if (!tile_alloc[tl] || (WF[tl * kTileWords] & WF_YOUNG)) continue;
+                if (!tile_alloc[tl] || (WF[tl * kTileWords] & WF_YOUNG) PULL_DIAG_SKIP(tl)) continue;
                 const uint32_t tw = tl >> 6;
                 if (tw != group_tw) {  // a pass never straddles two occupancy words
                     flush();
@@ -1982,7 +1982,7 @@ int gossip_engine::tick_step_a(int64_t t) {
         std::memset(TM, 0, (size_t)TM_WORDS * ntw * 8);
         const uint32_t ntiles = hw / kTileWords;
         for (uint32_t tl = 0; tl < ntiles; tl++) {
-            if (!tile_alloc[tl] || (WF[tl * kTileWords] & WF_YOUNG)) continue;  // not listed
+            if (!tile_alloc[tl] || (WF[tl * kTileWords] & WF_YOUNG) PULL_DIAG_SKIP(tl)) continue;  // not listed
             const unsigned long long bit = 1ull << (tl & 63u);
             unsigned long long* m = TM + (size_t)TM_WORDS * (tl >> 6);
             const bool fresh = tile_first[tl] == t;

@@ -702,3 +702,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP ? 5 : 1)
     }
 #undef PULL_LANES
 }
+
+// Diagnostic build only (Makefile engine_sk.o; results are WRONG there): tiles at least
+// GOSSIP_DIAG_SKIP_AGE ticks old are left out of k_pull's lists, to price the passes over the
+// previous generations' straggler tiles.  The product build leaves the lists as they are.
+#ifdef PULL_DIAG_SKIP_ENV
+#include <cstdlib>
+static inline bool diag_skip_tile(int64_t age) {
+    static const long a = std::getenv("GOSSIP_DIAG_SKIP_AGE") ? std::atol(std::getenv("GOSSIP_DIAG_SKIP_AGE")) : 0;
+    return a > 0 && age >= a;
+}
+#define PULL_DIAG_SKIP(tl) || diag_skip_tile(t - tile_first[tl])
+#else
+#define PULL_DIAG_SKIP(tl)
+#endif
