@@ -300,9 +300,20 @@ def rehearse_rows(args, wl, topo, ev, shards, R, flags):
 
 def resolve_shard_rule(rule, shards):
     """--shard-rule auto: the birth-tick rule from 8 share shards on, the hash rule below (one-rank
-    rehearsals, DESIGN.md section 5: 8 shards 24.8 vs 27.6 ms per tick; 4 shards 39.8 vs 36.7;
+    rehearsals, DESIGN.md section 5: 8 shards 24.8 vs 27.6 ms per tick, 22.1 with the tick rule's
+    fresh tile per birth tick (shard_flags); 4 shards 39.8 vs 36.7;
     2 shards: the tick rule's window peaks overflow the capacity estimate)."""
     return rule if rule != "auto" else ("tick" if shards >= 8 else "hash")
+
+
+def shard_flags(rule):
+    """Engine flags of a resolved shard rule.  The birth-tick rule also opens a fresh tile per
+    birth tick (GOSSIP_F_TILE_PER_TICK): a shard's births of one tick then never share a tile with
+    its births 8 ticks later, so every tile stays single-age -- young while its shares are young,
+    one age for the early exit, saturation bits and dense rows (one rank of 8: 22.1 vs 24.8 ms per
+    tick, same edge events).  The hash rule keeps the packed tiles (C4's 2
+    shards: 58.67 vs 58.15 ms per shard-tick with fresh tiles)."""
+    return (gossip.F_SHARD_BY_TICK | gossip.F_TILE_PER_TICK) if rule == "tick" else 0
 
 
 def main():
@@ -395,7 +406,7 @@ def main():
         err = None
         try:
             acc = run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank,
-                             flags | (gossip.F_SHARD_BY_TICK if shard_rule(shards) == "tick" else 0))
+                             flags | shard_flags(shard_rule(shards)))
         except gossip.GossipError as e:
             if getattr(e, "code", None) not in CAPACITY_CODES:
                 raise
@@ -471,6 +482,7 @@ def main():
                 "device_gib": acc["dev_bytes"] / 2**30,
                 "parallelism": f"share-shard x{shards} over {max(world, 1)} rank(s)",
                 "shard_rule": shard_rule(shards),
+                "fresh_tile_per_tick": bool(shard_flags(shard_rule(shards)) & gossip.F_TILE_PER_TICK),
             },
             "roofline": None,
         }

@@ -167,8 +167,9 @@ typedef struct gossip_config {
                               results are identical, only the bytes read change       */
 /* (flag values 8 and 16 -- the round-1 scalar-peer pull kernel and its opposite -- are retired
  *  and ignored) */
-#define GOSSIP_F_TILE_PER_TICK 32u /* test: open a fresh 1024-share tile every tick (wide,
-                                      sparsely filled windows at small n)                 */
+#define GOSSIP_F_TILE_PER_TICK 32u /* open a fresh 1024-share tile every tick: tests (wide,
+                                      sparsely filled windows at small n) and the birth-tick
+                                      share shards (bench.py shard_flags: single-age tiles) */
 #define GOSSIP_F_HOP_BATCH 128u /* hop-batched run: generation g of every node is simulated in
                                    batched tick g (its phase kept) and the cut / snapshots are
                                    applied per share from the real times -- exact when no two

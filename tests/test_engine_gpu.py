@@ -288,20 +288,22 @@ def test_early_retire_near_capacity(gossip, oracle):
         assert np.array_equal(getattr(st, k), getattr(r, k)), k
 
 
-@pytest.mark.parametrize("rule", ["hash", "birth_tick"])
+@pytest.mark.parametrize("rule", ["hash", "birth_tick", "birth_tick_fresh_tiles"])
 def test_sharded_engines_sum_to_whole(gossip, rule):
     n = 5000
     topo = gossip.Topology.gnp(n, 12.0 / (n - 1), 31, gossip.TOPO_SKIP)
     t_cut = gossip.seconds_to_ns(9.9)
     ev = gossip.make_schedule(n, 77, T0, t_cut, id_mask=0xFFFF)
     whole = _engine_for(gossip, topo, ev, L, t_cut).stats()
-    fl = gossip.F_SHARD_BY_TICK if rule == "birth_tick" else 0
+    # (bench.shard_flags: the birth-tick rule runs with a fresh tile per birth tick)
+    fl = {"hash": 0, "birth_tick": gossip.F_SHARD_BY_TICK,
+          "birth_tick_fresh_tiles": gossip.F_SHARD_BY_TICK | gossip.F_TILE_PER_TICK}[rule]
     parts = [_engine_for(gossip, topo, ev, L, t_cut, flags=fl, shard_rank=r, shard_count=3).stats()
              for r in range(3)]
     for k in ("gen", "recv", "fwd", "sent", "processed"):
         tot = sum(getattr(s, k).astype(np.uint64) for s in parts)
         assert np.array_equal(tot, getattr(whole, k).astype(np.uint64)), k
-    owner = gossip.shard_events(topo, ev, 3, by_tick_latency_ns=L if fl else 0)
+    owner = gossip.shard_events(topo, ev, 3, by_tick_latency_ns=L if fl & gossip.F_SHARD_BY_TICK else 0)
     for r in range(3):
         assert np.array_equal(np.bincount(ev["node"][owner == r], minlength=n), parts[r].gen)
 

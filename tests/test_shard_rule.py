@@ -70,3 +70,6 @@ def test_bench_auto_rule_takes_birth_ticks_from_8_shards():
     spec.loader.exec_module(bench)
     assert [bench.resolve_shard_rule("auto", s) for s in (1, 2, 4, 8, 16)] == ["hash", "hash", "hash", "tick", "tick"]
     assert bench.resolve_shard_rule("hash", 8) == "hash" and bench.resolve_shard_rule("tick", 2) == "tick"
+    # the birth-tick rule opens a fresh tile per birth tick; the hash rule packs tiles
+    assert bench.shard_flags("tick") == bench.gossip.F_SHARD_BY_TICK | bench.gossip.F_TILE_PER_TICK
+    assert bench.shard_flags("hash") == 0
