@@ -306,14 +306,17 @@ def resolve_shard_rule(rule, shards):
     return rule if rule != "auto" else ("tick" if shards >= 8 else "hash")
 
 
-def shard_flags(rule):
+def shard_flags(rule, fresh="auto"):
     """Engine flags of a resolved shard rule.  The birth-tick rule also opens a fresh tile per
     birth tick (GOSSIP_F_TILE_PER_TICK): a shard's births of one tick then never share a tile with
     its births 8 ticks later, so every tile stays single-age -- young while its shares are young,
     one age for the early exit, saturation bits and dense rows (one rank of 8: 22.1 vs 24.8 ms per
     tick, same edge events).  The hash rule keeps the packed tiles (C4's 2
     shards: 58.67 vs 58.15 ms per shard-tick with fresh tiles)."""
-    return (gossip.F_SHARD_BY_TICK | gossip.F_TILE_PER_TICK) if rule == "tick" else 0
+    f = gossip.F_SHARD_BY_TICK if rule == "tick" else 0
+    if fresh == "on" or (fresh == "auto" and rule == "tick"):  # (--fresh-tiles: A/B override)
+        f |= gossip.F_TILE_PER_TICK
+    return f
 
 
 def main():
@@ -336,6 +339,9 @@ def main():
                          "generation (GOSSIP_F_SHARD_BY_TICK: a shard's births of a tick fill whole "
                          "tiles of one age); auto (default): tick from 8 shards on, hash below "
                          "(DESIGN.md section 5: measured one-rank rehearsals)")
+    ap.add_argument("--fresh-tiles", choices=["auto", "on", "off"], default="auto",
+                    help="a fresh tile per birth tick (GOSSIP_F_TILE_PER_TICK); auto (default): with "
+                         "the tick rule only (shard_flags)")
     ap.add_argument("--rehearse-rows", type=int, default=0,
                     help="diagnostic: one rank of an R-rank row partition of share shard 0 of "
                          "--rehearse-shards (default: the workload's fit) on this one GPU")
@@ -406,7 +412,7 @@ def main():
         err = None
         try:
             acc = run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank,
-                             flags | shard_flags(shard_rule(shards)))
+                             flags | shard_flags(shard_rule(shards), args.fresh_tiles))
         except gossip.GossipError as e:
             if getattr(e, "code", None) not in CAPACITY_CODES:
                 raise
@@ -482,7 +488,7 @@ def main():
                 "device_gib": acc["dev_bytes"] / 2**30,
                 "parallelism": f"share-shard x{shards} over {max(world, 1)} rank(s)",
                 "shard_rule": shard_rule(shards),
-                "fresh_tile_per_tick": bool(shard_flags(shard_rule(shards)) & gossip.F_TILE_PER_TICK),
+                "fresh_tile_per_tick": bool(shard_flags(shard_rule(shards), args.fresh_tiles) & gossip.F_TILE_PER_TICK),
             },
             "roofline": None,
         }

@@ -73,3 +73,5 @@ def test_bench_auto_rule_takes_birth_ticks_from_8_shards():
     # the birth-tick rule opens a fresh tile per birth tick; the hash rule packs tiles
     assert bench.shard_flags("tick") == bench.gossip.F_SHARD_BY_TICK | bench.gossip.F_TILE_PER_TICK
     assert bench.shard_flags("hash") == 0
+    assert bench.shard_flags("hash", "on") == bench.gossip.F_TILE_PER_TICK
+    assert bench.shard_flags("tick", "off") == bench.gossip.F_SHARD_BY_TICK
