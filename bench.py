@@ -48,7 +48,16 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # variant -- these values, the resolved young grid and the library build -- equals the pass's
 LAUNCH_OPTIONS = ("pull_nt", "pull_grid", "pull_gate", "pull_tiles", "pull_tile_order",
                   "pull_sat", "dense_rows", "late_age", "young", "young_age", "young_cap",
-                  "young_list_cap", "young_nt", "young_overlap", "young_grid")
+                  "young_list_cap", "young_nt", "young_overlap", "young_grid", "young_skip")
+
+
+def option_or_none(eng, name):
+    """An engine option's value, or None when the loaded library predates the option (A/B runs
+    against an earlier build)."""
+    try:
+        return eng.get_option(name)
+    except gossip.GossipError:
+        return None
 
 
 def lib_build_id():
@@ -176,7 +185,7 @@ def run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank, fl
         t_eng = time.perf_counter()
         eng = gossip.Engine(wl["nodes"], L_NS, T0_NS, T_CUT_NS, device=local, flags=flags,
                             shard_rank=s, shard_count=shards)
-        acc["options"] = {k: eng.get_option(k) for k in LAUNCH_OPTIONS}
+        acc["options"] = {k: option_or_none(eng, k) for k in LAUNCH_OPTIONS}
         try:
             eng.set_topology(topo)
             eng.set_schedule(ev)
@@ -342,6 +351,10 @@ def main():
     ap.add_argument("--fresh-tiles", choices=["auto", "on", "off"], default="auto",
                     help="a fresh tile per birth tick (GOSSIP_F_TILE_PER_TICK); auto (default): with "
                          "the tick rule only (shard_flags)")
+    ap.add_argument("--rehearse-index", type=int, default=0,
+                    help="diagnostic, with --rehearse-shards S: the shard (rank) to rehearse, or -1 for "
+                         "every rank 0..S-1 one after another (the line then reports each rank's time "
+                         "and the job's tick = the slowest rank's)")
     ap.add_argument("--rehearse-rows", type=int, default=0,
                     help="diagnostic: one rank of an R-rank row partition of share shard 0 of "
                          "--rehearse-shards (default: the workload's fit) on this one GPU")
@@ -407,12 +420,22 @@ def main():
     while True:
         shards = passes * world
         my_shards = [rank * passes + q for q in range(passes)]
-        if rehearsal:  # shard 0 of S (S doubled with passes if it does not fit)
-            shards, my_shards = args.rehearse_shards * (passes // max(1, -(-wl["fit_shards"] // world))), [0]
+        rank_accs = []
+        if rehearsal:  # shard I of S (S doubled with passes if it does not fit)
+            shards = args.rehearse_shards * (passes // max(1, -(-wl["fit_shards"] // world)))
+            my_shards = [args.rehearse_index] if args.rehearse_index >= 0 else list(range(shards))
+            if any(s >= shards for s in my_shards):
+                raise SystemExit(f"--rehearse-index {args.rehearse_index}: only {shards} shards")
         err = None
         try:
-            acc = run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank,
-                             flags | shard_flags(shard_rule(shards), args.fresh_tiles))
+            if rehearsal:  # one engine per rehearsed rank, in sequence (each its own timed window)
+                for s in my_shards:
+                    rank_accs.append(run_shards(args, wl, topo, ev, [s], shards, dist, dev, local, rank,
+                                                flags | shard_flags(shard_rule(shards), args.fresh_tiles)))
+                acc = max(rank_accs, key=lambda a: a["elapsed"])  # the job waits for its slowest rank
+            else:
+                acc = run_shards(args, wl, topo, ev, my_shards, shards, dist, dev, local, rank,
+                                 flags | shard_flags(shard_rule(shards), args.fresh_tiles))
         except gossip.GossipError as e:
             if getattr(e, "code", None) not in CAPACITY_CODES:
                 raise
@@ -429,7 +452,10 @@ def main():
     layout = (f"{shards} share shards, {len(my_shards)} per GPU in sequence" if len(my_shards) > 1
               else f"{shards} share shards, one per GPU")
     if rehearsal:
-        wl["desc"] += f" [REHEARSAL: shard 0 of {shards} on one GPU]"
+        which = (f"shard {my_shards[0]}" if len(my_shards) == 1 else
+                 f"shards 0..{shards - 1} one after another, the slowest one's window")
+        wl["desc"] += f" [REHEARSAL: {which} of {shards} on one GPU]"
+        layout = f"{shards} share shards, one per GPU"
 
     elapsed, edges, pull_ms = acc["elapsed"], acc["edges"], acc["pull_ms"]
     launches = acc["launches"]
@@ -492,6 +518,18 @@ def main():
             },
             "roofline": None,
         }
+        if rehearsal:
+            out["config"]["rehearsed_shards"] = my_shards
+            if len(rank_accs) > 1:  # every rank's timed window: ms per tick, window peak, edges
+                out["config"]["rank_ms_per_step"] = [a["elapsed"] * 1e3 / K for a in rank_accs]
+                out["config"]["rank_live_words"] = [a["words_hw"] for a in rank_accs]
+                out["config"]["rank_window_capacity_words"] = [a["words_cap"] for a in rank_accs]
+                out["config"]["rank_edge_events"] = [a["edges"] for a in rank_accs]
+                out["config"]["rank_phase_ms_per_tick"] = [a["phase_ms"] / max(a["launches"], 1) for a in rank_accs]
+                out["config"]["edge_events_all_ranks"] = int(sum(a["edges"] for a in rank_accs))
+                # what an S-GPU job of these ranks would reach (unmeasured on an S-GPU node): every
+                # rank's edge events over the slowest rank's window
+                out["config"]["projected_job_value"] = out["config"]["edge_events_all_ranks"] / elapsed
         k_pull = {
             "kernel": "k_pull",
             "avg_launch_ms": avg_ms,

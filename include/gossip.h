@@ -302,6 +302,18 @@ uint32_t gossip_share_message_length(uint32_t origin, uint32_t share_id, int64_t
  *                      to dense seen rows (tests: small lists exercise the overflow paths)
  *   "young_nt"         1: k_pull_young reads its peers' slot lines non-temporally (default), 0:
  *                      cached                                                  [GOSSIP_YOUNG_NT]
+ *   "pull_push"        push marks: rows of tiles whose next frontier sits on few nodes mark their
+ *                      writers' peers, and the next tick's k_pull skips those tiles at unmarked
+ *                      nodes; -1 auto (BFS layer model: marked nodes expected < 50 %, default), 0
+ *                      off, 1 every listed tile that is not dense-row (tests)  [GOSSIP_PULL_PUSH]
+ *   "young_idle"       1: on a tick whose k_pull_young reads only stamped slots and keeps every seen
+ *                      list, nodes without a stamped peer skip the per-node walk (default), 0: off
+ *                                                                          [GOSSIP_YOUNG_IDLE]
+ *   "young_skip"       empty-slot skipping: on a tick whose slots are expected mostly empty, every
+ *                      writer of a non-empty slot stamps its peers' hint bytes and the next tick's
+ *                      k_pull_young loads only the stamped peers' slot lines; -1 auto (the BFS
+ *                      layer model expects < 30 % of the slots non-empty, default), 0 off, 1 every
+ *                      tick (tests)                                          [GOSSIP_YOUNG_SKIP]
  *   "young_overlap"    0: k_pull_young after k_pull on the engine stream; 1: the two run
  *                      concurrently on two streams, k_pull_young launched first (default)
  *                                                                   [GOSSIP_YOUNG_OVERLAP]
@@ -359,8 +371,9 @@ typedef struct gossip_counters {
     uint64_t pull_bytes_moved; /* bytes the pull kernels actually had to move after
                                   dead-word / saturated-node skipping (since reset)   */
     uint64_t pull_pair_edges;  /* (edge, 16-B word pair) neighbour reads (since reset) */
-    uint64_t dense_ops;        /* DENSE mode: int8 MAC ops x2 of the MFMA tiles computed
-                                  = 2 * 128 * 128 * n_pad per 128x128 output tile       */
+    uint64_t dense_ops;        /* DENSE mode: int8 MAC ops x2 of the MFMA work computed =
+                                  2 * 256 * 256 * 1024 per (256x256 output tile, 1,024-node K
+                                  stage) computed; empty stages are skipped, not counted */
     uint64_t dense_tiles_skipped; /* DENSE mode: output tiles skipped as dead           */
     /* pull traffic breakdown since reset (each a count of the unit in brackets):         */
     uint64_t pull_col_ids;     /* peer ids loaded [4 B]                                 */
@@ -408,7 +421,13 @@ typedef struct gossip_counters {
                                       transposed F_next) since creation; the others ran k_transpose,
                                       k_dense_bits and k_dense_dedup (option dense_fused)       */
     uint32_t young_grid;         /* blocks of the last k_pull_young launch (option young_grid resolved) */
-    uint32_t pad1;
+    uint32_t young_skip_ticks;   /* k_pull_young launches that read only stamped slots (young_skip) since reset */
+    /* push marks (option pull_push) since reset: (tile, tick) pairs k_pull skipped at unmarked nodes,
+       (tile, tick) pairs whose rows marked their writers' peers, and marks set (8-B atomics) */
+    uint64_t pull_push_tiles;
+    uint64_t pull_pushw_tiles;
+    uint64_t pull_marks;
+    uint64_t young_idle_ticks;   /* k_pull_young launches that skipped their idle nodes' walks (young_idle) */
 } gossip_counters;
 int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c);
 /* Option rehearse_rows = R: per row block r < R, summed since the last reset_timing -- pull time,

@@ -132,6 +132,11 @@ struct PullArgs {
     // words (null: off); tmask[TM_WORDS * tw + TM_*] the tick's per-occupancy-word tile masks.
     unsigned long long* sat = nullptr;
     const unsigned long long* tmask = nullptr;
+    // Push marks (round 6, option pull_push; pull_kernel.h): bit v of mark_cur says some peer of v
+    // wrote a non-empty F_cur row of a TM_PUSH tile (the tiles whose frontier the host expects on
+    // few nodes); this tick's rows of TM_PUSHW tiles mark their writer's peers in mark_next.
+    const unsigned long long* mark_cur = nullptr;
+    unsigned long long* mark_next = nullptr;
 };
 
 // Phase-ordered update of id groups inside one word (rare: only words holding groups).
@@ -167,7 +172,7 @@ __device__ __forceinline__ uint64_t group_fix(uint64_t nw, uint64_t seen, uint64
 // separate 128-B lines and summed on the host.  Every wave adds its own counts at its end; with a
 // single copy, thousands of waves finishing together queue their atomics on ONE L2 line and wait
 // for them at the next barrier (k_dense_dedup: 4,096 waves x 3 atomics = ~100 us per C2 dispatch).
-constexpr uint32_t kAcctSlots = 32, kAcctReplicas = 64;
+constexpr uint32_t kAcctSlots = 40, kAcctReplicas = 64;
 __device__ __forceinline__ void acct_add(unsigned long long* acct, uint32_t slot, unsigned long long v) {
     atomicAdd(&acct[(blockIdx.x & (kAcctReplicas - 1u)) * kAcctSlots + slot], v);
 }
@@ -243,16 +248,19 @@ uint64_t pull_grid_cap(bool nt, int64_t ov) {
 // profiles/r04/ab/r4l_*); the option that selected them was removed in round 5.
 constexpr int kWideLanes = 32;
 
+bool pull_sp(int lpw, int epn, const PullArgs& a);
 template <int LPW, int EPN>
 void launch_pull_t(bool nt, uint32_t grid, size_t lds, hipStream_t s, const PullArgs& a) {
     if constexpr (LPW == 32 && EPN == 1) {
-        // the flags k_pull<.., SP = true> takes as compile-time constants (pull_kernel.h): the
-        // same conditions the kernel derives at run time
-        const bool sp = a.tmask != nullptr && a.ptile != nullptr && a.sat != nullptr &&
-                        a.nptile / (uint32_t)(LPW / 8) <= kPullMaxPasses && !a.noskip && a.gate_seen;
-        if (sp) {
-            if (nt)
+        if (pull_sp(LPW, EPN, a)) {
+            // push marks in their own instantiation (the other one keeps its register allocation)
+            const bool push = a.mark_cur != nullptr || a.mark_next != nullptr;
+            if (nt && push)
+                k_pull<LPW, 1, true, true, true><<<grid, 256, lds, s>>>(a);
+            else if (nt)
                 k_pull<LPW, 1, true, true><<<grid, 256, lds, s>>>(a);
+            else if (push)
+                k_pull<LPW, 1, false, true, true><<<grid, 256, lds, s>>>(a);
             else
                 k_pull<LPW, 1, false, true><<<grid, 256, lds, s>>>(a);
             return;
@@ -265,6 +273,13 @@ void launch_pull_t(bool nt, uint32_t grid, size_t lds, hipStream_t s, const Pull
         }
     }
     if constexpr (LPW * EPN <= 64) k_pull<LPW, EPN><<<grid, 256, lds, s>>>(a);
+}
+
+// the flags k_pull<.., SP = true> takes as compile-time constants (pull_kernel.h): the same
+// conditions the kernel derives at run time.  Push marks (PullArgs::mark_*) run only there.
+bool pull_sp(int lpw, int epn, const PullArgs& a) {
+    return lpw == 32 && epn == 1 && a.tmask != nullptr && a.ptile != nullptr && a.sat != nullptr &&
+           a.nptile / (uint32_t)(lpw / 8) <= kPullMaxPasses && !a.noskip && a.gate_seen;
 }
 
 template <int LPW>
@@ -325,6 +340,13 @@ struct BirthArgs {
     const int32_t* rev;
     uint8_t* hint_next;
     uint32_t stamp_next;
+    uint32_t stamp1_next;      // sparse_wr: a birth that makes its slot non-empty stamps it too
+    // push marks (pull_kernel.h): a birth into a push-write tile (tmask TM_PUSHW) marks its node's
+    // peers, as k_pull does for the rows it writes (null: no push-write tile this tick)
+    unsigned long long* mark_next;
+    const unsigned long long* tmask;
+    const int32_t* col;
+    uint32_t sparse_wr;
     uint16_t* list;            // young tiles: seen lists (young_kernel.h)
     const uint8_t* wt_yid;     // write-sparse index -> young id, this tick
     uint32_t list_max;         // entries a list holds (kListU16 - 1; option young_list_cap)
@@ -453,6 +475,9 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
                 if (a.hint_next)  // and the readers of the next tick load it
                     for (int64_t j = a.rowptr[v]; j < a.rowptr[v + 1]; j++)
                         if (a.rev[j] >= 0) a.hint_next[a.rev[j]] = (uint8_t)a.stamp_next;
+            } else if (hdr == 0u && a.sparse_wr && a.hint_next) {  // (young_kernel.h, empty-slot
+                for (int64_t j = a.rowptr[v]; j < a.rowptr[v + 1]; j++)  //  skipping: now non-empty)
+                    if (a.rev[j] >= 0) a.hint_next[a.rev[j]] = (uint8_t)a.stamp1_next;
             }
         }
         if (lovf) {
@@ -515,6 +540,11 @@ __global__ __launch_bounds__(256) void k_births(BirthArgs a) {
         } else {
             *fp |= bit;
         }
+        if (a.mark_next && ((a.tmask[(uint64_t)TM_WORDS * (tile >> 6) + TM_PUSHW] >> (tile & 63u)) & 1ull))
+            for (int64_t j = a.rowptr[v]; j < a.rowptr[v + 1]; j++) {
+                const uint32_t u = (uint32_t)a.col[j];
+                atomicOr(&a.mark_next[u >> 6], 1ull << (u & 63u));
+            }
         *sp |= bit;
         a.effgen[v] += 1u;
         atomicOr(&a.live[w], (unsigned long long)bit);
@@ -621,10 +651,20 @@ constexpr int kLag = 2;    // ticks of lag before liveness is read back
 // shuffles per peer batch: C4 1.179e13 -> 1.259e13 edge events/s (peer rows 274 -> 216 GB per
 // launch, ages 7/8 alone give the same), C3 3.11 -> 3.07 ms per tick (profiles/r02/late_ab.txt)
 constexpr int64_t kAutoLateAge = 1;
+// young_skip auto: stamp non-empty slots when under this fraction of them is expected non-empty
+// (a stamp costs a writer a byte store per peer; a skipped peer saves its reader a 128-B line)
+constexpr double kSkipSlotFrac = 0.3;
+// pull_push auto: a tile's F_next rows mark their peers when the marked nodes are expected to be
+// under this fraction of all (an unmarked node skips the tile: no own-seen read, no occupancy words)
+constexpr double kPushFrac = 0.5;
 constexpr double kYoungMinEntries = 16.0;  // young auto: expected slot entries per node (see alloc_device)
 constexpr uint32_t kTileWords = 16;  // allocation unit: 16 words = 1024 shares = 128 B per row
-// second-line hint stamp of tick t (young_kernel.h): never 0, the value hint bytes start with
-inline uint32_t hint_stamp(int64_t t) { return 1u + (uint32_t)(((t % 255) + 255) % 255); }
+// hint stamps of tick t (young_kernel.h), never 0 (the value hint bytes start with): a second
+// line, 129..255; (empty-slot skipping) a non-empty slot of one line, 1..127.  A byte keeps its
+// value until its writer stamps it again, so a stale byte can match only 254 ticks later (127 is
+// odd: the same frontier buffer), and a stale match only costs a line read.
+inline uint32_t hint_stamp1(int64_t t) { return 1u + (uint32_t)(((t % 127) + 127) % 127); }
+inline uint32_t hint_stamp(int64_t t) { return 0x80u | hint_stamp1(t); }
 
 }  // namespace
 
@@ -784,6 +824,29 @@ struct gossip_engine {
     // bits written before a tick that listed the tile without them
     std::vector<int64_t> tile_satw;
     std::vector<int64_t> tile_dw;          // last tick every node's F_next row of the tile was written
+    // push marks (pull_kernel.h, option pull_push): -1 auto (the BFS layer model expects the rows of
+    // a tile's F_next on few enough nodes that their peers are under kPushFrac of all), 0 off, 1 every
+    // listed tile that is not dense-row (tests)
+    int64_t opt_pull_push = -1;
+    std::vector<int64_t> tile_pushw;       // last tick k_pull marked the peers of the tile's row writers
+    // per tile (this life): (tick, generations) of the births that landed in it -- its frontier by
+    // the layer model is the sum of their floods (an old tile can take a late generation of an id
+    // instance it holds: one young flood among stragglers)
+    std::vector<std::vector<std::pair<int64_t, uint32_t>>> tile_births;
+    void note_birth(uint32_t tl, int64_t t) {
+        auto& h = tile_births[tl];
+        if (!h.empty() && h.back().first == t)
+            h.back().second++;
+        else
+            h.emplace_back(t, 1u);
+    }
+    unsigned long long* d_mark[2] = {nullptr, nullptr};  // per tick parity: bit v = v is marked
+    uint64_t push_tiles = 0, pushw_tiles = 0;  // (tile, tick) pairs read / written as push tiles since reset
+    int64_t mark_tick = INT64_MIN;         // the tick whose k_pull wrote d_mark[tick & 1]
+    uint64_t mark_launches = 0;            // k_pull launches that read a mark bitmap since reset
+    bool push_write(uint32_t tl, int64_t t) const;
+    // expected F_next entries per node of tile tl at tick t (BFS layer model over its births)
+    double frontier_entries(uint32_t tl, int64_t t) const;
     std::vector<int64_t> tile_inj_prev;    // the injection tick before tile_last_inject
     std::vector<uint32_t> tile_cols;       // columns allocated in the tile (this life)
     std::vector<double> hop_front;         // expected frontier fraction per hop (BFS layer model)
@@ -797,6 +860,13 @@ struct gossip_engine {
         }
     }
     int64_t opt_young_nt = 1;         // k_pull_young reads peers' slot lines non-temporally
+    // empty-slot skipping (young_kernel.h): -1 auto (the BFS layer model expects fewer than
+    // kSkipSlotFrac of the slots written this tick to be non-empty), 0 off, 1 every tick (tests)
+    int64_t opt_young_skip = -1;
+    bool skip_wr_last = false;        // last tick's slot writers stamped non-empty slots
+    uint64_t skip_ticks = 0;          // ticks whose k_pull_young read only stamped slots
+    int64_t opt_young_idle = 1;       // 1: k_pull_young's idle-node chunk pass (young_kernel.h), 0: off
+    uint64_t idle_ticks = 0;          // k_pull_young launches with the idle-node pass
     int64_t opt_young_list_cap = kListU16 - 1;  // seen-list entries (tests: small lists overflow)
     int64_t opt_late_age = -1;        // k_pull early exit for tiles >= this many ticks old (0: off, -1: auto)
     int64_t late_age_now() const {    // auto: every tile of a gathering (CSR) pull
@@ -819,6 +889,7 @@ struct gossip_engine {
     std::vector<uint8_t> tile_yid;             // young id of a young tile (kYidNone: not young)
     uint64_t yid_used = 0;                     // young ids in use (0 .. 62)
     uint16_t* d_ylist = nullptr;               // n x kListU16 seen lists (young_kernel.h)
+    unsigned long long* d_ywork = nullptr;     // per 64-node chunk: nodes with work (k_young_idle)
     YoungPack* h_young[kRing] = {};
     YoungPack* d_young[kRing] = {};
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timers_young;
@@ -934,7 +1005,7 @@ gossip_engine::~gossip_engine() {
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
     hipFree(d_rowptr_c); hipFree(d_col_c); hipFree(d_degc);
     for (int k = 0; k < 4; k++) { hipFree(d_smask[k]); hipHostFree(h_smask[k]); }
-    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen_mem); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_sat); hipFree(d_Ab); hipFree(d_FT[0]); hipFree(d_FT[1]); hipFree(d_snz[0]); hipFree(d_snz[1]); hipFree(d_snz[2]); hipFree(d_tix); hipFree(d_inc);
+    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen_mem); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_sat); hipFree(d_mark[0]); hipFree(d_mark[1]); hipFree(d_Ab); hipFree(d_FT[0]); hipFree(d_FT[1]); hipFree(d_snz[0]); hipFree(d_snz[1]); hipFree(d_snz[2]); hipFree(d_tix); hipFree(d_inc);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent); hipFree(d_phase_ts);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     hipFree(d_msg); hipFree(d_cnt); hipFree(d_scan_tmp); hipFree(d_recv_msgs); hipFree(d_sizes);
@@ -942,7 +1013,7 @@ gossip_engine::~gossip_engine() {
     for (int k = 0; k < kRing; k++) { hipFree(d_ptile[k]); hipHostFree(h_ptile[k]); }
     for (int k = 0; k < kRing; k++) { hipFree(d_tmask[k]); hipHostFree(h_tmask[k]); }
     hipFree(d_slot[0]); hipFree(d_slot[1]);
-    hipFree(d_rev); hipFree(d_hint[0]); hipFree(d_hint[1]); hipFree(d_ylist);
+    hipFree(d_rev); hipFree(d_hint[0]); hipFree(d_hint[1]); hipFree(d_ylist); hipFree(d_ywork);
     for (int k = 0; k < kRing; k++) { hipFree(d_young[k]); hipHostFree(h_young[k]); }
     for (auto& p : timers_young) {
         hipEventDestroy(p.first);
@@ -1248,6 +1319,11 @@ int gossip_engine::alloc_device() {
             HIP_TRY(hipMalloc(&d_sat, nzb));
             HIP_TRY(hipMemsetAsync(d_sat, 0, nzb, stream));
         }
+        if (!dense && row_count == 1 && !handshake)  // push marks: a bit per node and tick parity
+            for (int k = 0; k < 2; k++) {
+                HIP_TRY(hipMalloc(&d_mark[k], ((size_t)n + 64) / 64 * 8));
+                HIP_TRY(hipMemsetAsync(d_mark[k], 0, ((size_t)n + 64) / 64 * 8, stream));
+            }
     }
     {  // BFS layer model for the dense-row tiles: frontier fraction per hop of one flood
         hop_front.clear();
@@ -1289,8 +1365,10 @@ int gossip_engine::alloc_device() {
             HIP_TRY(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(d_slot[k]), (unsigned short)kSlotTomb,
                                       (size_t)n * kSlotU16, stream));
             HIP_TRY(hipMemset2DAsync(d_slot[k], kSlotU16 * 2u, 0, 2, n, stream));
-            HIP_TRY(hipMalloc(&d_hint[k], std::max<size_t>(nnz, 1)));
-            HIP_TRY(hipMemsetAsync(d_hint[k], 0, std::max<size_t>(nnz, 1), stream));  // stamps are >= 1
+            // (+16: the idle-node pass reads whole 4-B words of it)
+            if (k == 0) HIP_TRY(hipMalloc(&d_ywork, ((size_t)n + 127) / 64 * 8));
+            HIP_TRY(hipMalloc(&d_hint[k], (size_t)nnz + 16));
+            HIP_TRY(hipMemsetAsync(d_hint[k], 0, (size_t)nnz + 16, stream));  // stamps are >= 1
         }
         {  // reverse edges: rev[j] = the entry of v in the list of u = col[j] (j in v's list)
             std::vector<int32_t> rev(nnz, -1), perm(nnz);
@@ -1378,6 +1456,8 @@ int gossip_engine::alloc_device() {
     tile_listed.assign(stride / kTileWords, INT64_MIN);
     tile_satw.assign(stride / kTileWords, INT64_MIN);
     tile_dw.assign(stride / kTileWords, INT64_MIN);
+    tile_pushw.assign(stride / kTileWords, INT64_MIN);
+    tile_births.assign(stride / kTileWords, {});
     tile_inj_prev.assign(stride / kTileWords, INT64_MIN);
     tile_cols.assign(stride / kTileWords, 0u);
     word_insts.assign(stride, {});
@@ -1522,6 +1602,8 @@ int gossip_engine::grow(uint32_t new_stride) {
     tile_listed.resize(new_stride / kTileWords, INT64_MIN);
     tile_satw.resize(new_stride / kTileWords, INT64_MIN);
     tile_dw.resize(new_stride / kTileWords, INT64_MIN);
+    tile_pushw.resize(new_stride / kTileWords, INT64_MIN);
+    tile_births.resize(new_stride / kTileWords);
     tile_inj_prev.resize(new_stride / kTileWords, INT64_MIN);
     tile_cols.resize(new_stride / kTileWords, 0u);
     tile_widx.resize(new_stride / kTileWords, 0xffu);
@@ -1576,6 +1658,8 @@ int gossip_engine::alloc_bits(uint32_t k, uint32_t* word, uint8_t* lo, int64_t t
         tile_listed[tl] = INT64_MIN;
         tile_satw[tl] = INT64_MIN;
         tile_dw[tl] = INT64_MIN;
+        tile_pushw[tl] = INT64_MIN;
+        tile_births[tl].clear();
         for (uint32_t q = 0; q < kTileWords; q++) reset_now.push_back(tl * kTileWords + q);
         open_tile = tl;
         open_word_in_tile = 0;
@@ -1598,6 +1682,27 @@ bool gossip_engine::dense_row_hop(uint32_t tl, int64_t hop) const {
     if (opt_dense_rows == 1) return hop >= 1;
     if (hop < 0 || hop >= (int64_t)hop_front.size()) return false;
     return (double)tile_cols[tl] * hop_front[(size_t)hop] >= kDenseRowBits;
+}
+
+// Push marks (pull_kernel.h): does the F_next of tile tl at tick t sit on few enough nodes that
+// their peers -- the nodes that must pull the tile next tick -- are under kPushFrac of all?  BFS
+// layer model: a share born at tick b is at hop t - b in F_next and its frontier holds hop_front[t -
+// b] of the nodes (beyond the model's last hop: none -- stragglers); the tile's births together give
+// the expected frontier entries per node, each marks avg_deg nodes, and a node is marked with
+// probability 1 - e^-(marks per node).  A misjudged tile costs marking work, never results (a marked
+// node pulls the tile as before).
+double gossip_engine::frontier_entries(uint32_t tl, int64_t t) const {
+    double e = 0.0;
+    for (const auto& b : tile_births[tl]) {
+        const int64_t h = t - b.first;
+        if (h >= 0 && h < (int64_t)hop_front.size()) e += (double)b.second * hop_front[(size_t)h];
+    }
+    return e;
+}
+bool gossip_engine::push_write(uint32_t tl, int64_t t) const {
+    if (opt_pull_push == 1) return true;
+    const double avg_deg = n ? (double)nnz / n : 0.0;
+    return 1.0 - std::exp(-frontier_entries(tl, t) * avg_deg) < kPushFrac;
 }
 
 // High-water mark above which alloc_bits first retires from the freshest liveness (retire_early):
@@ -1710,6 +1815,7 @@ int gossip_engine::tick_step_a(int64_t t) {
                 }
             }
             mark_inject(I.word / kTileWords, t);
+            note_birth(I.word / kTileWords, t);
             b.col = I.word * 64u + I.lo + ev_rank[q];
             if (I.nsrc > 1) {
                 b.kind = BIRTH_GROUP;
@@ -1728,6 +1834,7 @@ int gossip_engine::tick_step_a(int64_t t) {
     //     write-sparse last tick) plus fresh tiles opened by this tick's births; the youngest of
     //     them stay (or become) write-sparse while their oldest shares are <= young_age hops old.
     uint32_t ny = 0, nwt = 0, ny_read = 0, ny_leave = 0;
+    bool skip_wr = false;  // this tick's slot writers stamp non-empty slots (young_skip)
     YoungPack* YP = young ? h_young[slot] : nullptr;
     std::vector<uint8_t> new_widx;
     if (young) {
@@ -1808,6 +1915,17 @@ int gossip_engine::tick_step_a(int64_t t) {
             const uint32_t tl = B[q].col >> 10;
             B[q].widx = tl < new_widx.size() ? new_widx[tl] : 0xffu;
             B[q].yid = B[q].widx != 0xffu ? tile_yid[tl] : kYidNone;
+        }
+        // empty-slot skipping: expected slot entries per node of F_next = sum over the write-sparse
+        // tiles of columns x frontier fraction at F_next's hop (t - first: births are hop 0), and a
+        // node's slot is non-empty with probability 1 - e^-entries
+        skip_wr = false;
+        if (opt_young_skip == 1) {
+            skip_wr = nwt > 0;
+        } else if (opt_young_skip == -1 && nwt) {
+            double e = 0.0;
+            for (uint32_t q = 0; q < nwt; q++) e += frontier_entries(YP->wt[q], t);
+            skip_wr = 1.0 - std::exp(-e) < kSkipSlotFrac;
         }
     } else {
         for (uint32_t q = 0; q < nb; q++) B[q].widx = 0xffu;
@@ -1966,6 +2084,9 @@ int gossip_engine::tick_step_a(int64_t t) {
     // Row partitions keep neither (another rank's rows arrive only where occupied).
     sat_used = sat_on;
     last_dense_tiles = 0;
+    // push marks ride on the saturation words (an unmarked node's push tiles read as saturated)
+    const bool push_on = sat_on && opt_pull_push != 0 && d_mark[0];
+    bool pushw_any = false;
     if (sat_used || dr_used) {
         if (TM_WORDS * ntw > tmask_cap) {
             HIP_TRY(hipStreamSynchronize(stream));
@@ -1981,6 +2102,19 @@ int gossip_engine::tick_step_a(int64_t t) {
         unsigned long long* TM = h_tmask[slot];
         std::memset(TM, 0, (size_t)TM_WORDS * ntw * 8);
         const uint32_t ntiles = hw / kTileWords;
+        // Push-write tiles only when the NEXT tick is expected light: every tile k_pull will list
+        // then (the listed ones now, the tiles leaving the young set now) has its F_next on few
+        // enough nodes (push_write) and none turns dense-row.  The k_pull instantiation that reads
+        // and writes marks holds more registers (pull_kernel.h PUSH): on a tick with dense tiles
+        // (every C4 tick at 2 shards) it costs more than it skips (58.4 -> 60.1 ms per phase).
+        bool light_next = push_on;
+        if (push_on && opt_pull_push != 1) {
+            for (uint32_t tl = 0; tl < ntiles && light_next; tl++)
+                if (tile_alloc[tl] && !(WF[tl * kTileWords] & WF_YOUNG))
+                    light_next = push_write(tl, t) && !(dr_used && dense_row_hop(tl, t - tile_first[tl]));
+            for (uint32_t i = 0; young && i < ny_leave && light_next; i++)
+                light_next = push_write(YP->yt[YP->lv[i]].tile, t);
+        }
         for (uint32_t tl = 0; tl < ntiles; tl++) {
             if (!tile_alloc[tl] || (WF[tl * kTileWords] & WF_YOUNG) PULL_DIAG_SKIP(tl)) continue;  // not listed
             const unsigned long long bit = 1ull << (tl & 63u);
@@ -1992,9 +2126,23 @@ int gossip_engine::tick_step_a(int64_t t) {
             // sat bits written by k_pull last tick, no birth since
             const bool clean = !fresh && tile_last_inject[tl] != t - 1 && tile_inj_prev[tl] != t - 1;
             if (sat_used && clean && tile_satw[tl] == t - 1) m[TM_SATOK] |= bit;
+            bool dw = false;
             if (dr_used && dense_row_hop(tl, t - tile_first[tl])) {  // F_cur's hop next tick
                 for (uint32_t q = 0; q < kTileWords; q++) WF[tl * kTileWords + q] |= (uint8_t)WF_DW;
                 tile_dw[tl] = t;
+                dw = true;
+            }
+            // push marks: the tile's F_cur rows were written by last tick's k_pull alone (listed then
+            // with TM_PUSHW, no birth since) -> skipped at unmarked nodes; this tick's rows mark
+            // peers when next tick's frontier is expected on few nodes
+            // (births of t - 1 into the tile marked their nodes' peers too: k_births)
+            if (push_on && !dr && !fresh && tile_pushw[tl] == t - 1) {
+                m[TM_PUSH] |= bit;
+                push_tiles++;
+            }
+            if (light_next && !dw && push_write(tl, t)) {  // (tile_pushw: set by the launch that marks)
+                m[TM_PUSHW] |= bit;
+                pushw_any = true;
             }
             tile_listed[tl] = t;
         }
@@ -2044,6 +2192,11 @@ int gossip_engine::tick_step_a(int64_t t) {
         b.rowptr = d_rowptr; b.rev = d_rev;
         b.hint_next = young ? d_hint[nxt] : nullptr;
         b.stamp_next = hint_stamp(t);
+        b.stamp1_next = hint_stamp1(t);
+        b.sparse_wr = skip_wr ? 1u : 0u;
+        b.mark_next = pushw_any ? d_mark[t & 1] : nullptr;
+        b.tmask = pushw_any ? d_tmask[slot] : nullptr;
+        b.col = d_col;
         b.list = d_ylist;
         b.list_max = (uint32_t)opt_young_list_cap;
         b.wt_yid = young ? d_young[slot]->wt_yid : nullptr;
@@ -2121,7 +2274,20 @@ int gossip_engine::tick_step_a(int64_t t) {
                 if (c.ptile && epn == 1 && (sat_used || dr_used)) {
                     c.tmask = d_tmask[slot];
                     c.sat = sat_used ? d_sat : nullptr;
-                    extra_lds = kPullSatLds;
+                    if (push_on && pull_sp(lpw, epn, c)) {  // marks of last tick's push-write rows / this tick's
+                        c.mark_cur = mark_tick == t - 1 ? d_mark[(t - 1) & 1] : nullptr;
+                        mark_launches += c.mark_cur != nullptr;
+                        c.mark_next = pushw_any ? d_mark[t & 1] : nullptr;
+                        // a tile is read as a push tile next tick only if a launch that marks
+                        // covered it (tile_pushw): the mark bitmap then holds every writer's peers
+                        if (c.mark_next)
+                            for (uint32_t tl = wb / kTileWords; tl < (wb + c.wact) / kTileWords; tl++)
+                                if ((h_tmask[slot][(size_t)TM_WORDS * (tl >> 6) + TM_PUSHW] >> (tl & 63u)) & 1ull) {
+                                    tile_pushw[tl] = t;
+                                    pushw_tiles++;
+                                }
+                    }
+                    extra_lds = kPullSatLds + ((c.mark_cur || c.mark_next) ? kPullPushLds : 0);
                     sat_launches += sat_used;
                     if (sat_used)  // this launch writes the sat bits of its listed tiles
                         for (uint32_t tl = wb / kTileWords; tl < (wb + c.wact) / kTileWords; tl++)
@@ -2173,6 +2339,8 @@ int gossip_engine::tick_step_a(int64_t t) {
             // k_pull writes whole occupancy words only for the words its listed tiles fall in
             HIP_TRY(hipMemsetAsync(d_nz[nxt] + (uint64_t)v0 * ntw, 0, (size_t)(v1 - v0) * ntw * 8u, stream));
         }
+        if (pushw_any)  // this tick's push marks start empty (last read by the pull of t - 1)
+            HIP_TRY(hipMemsetAsync(d_mark[t & 1], 0, ((size_t)n + 64) / 64 * 8, stream));
         if (cfg.flags & GOSSIP_F_TIMING) {
             e0 = get_event();
             e1 = get_event();
@@ -2196,6 +2364,17 @@ int gossip_engine::tick_step_a(int64_t t) {
             y.cap = (uint32_t)std::min<int64_t>(kSlotU16 - 1, std::max<int64_t>(1, opt_young_cap));
             y.hint_cur = d_hint[fcur]; y.hint_next = d_hint[nxt]; y.rev = d_rev;
             y.stamp_cur = hint_stamp(t - 1); y.stamp_next = hint_stamp(t);
+            y.stamp1_cur = hint_stamp1(t - 1); y.stamp1_next = hint_stamp1(t);
+            y.sparse_rd = (skip_wr_last && ny_read) ? 1u : 0u;  // (last tick's writers stamped)
+            y.sparse_wr = skip_wr ? 1u : 0u;
+            // idle nodes skip the node walk (young_kernel.h) when only stamped slots are read and
+            // every read tile stays young (no list entry is dropped or materialised)
+            bool stay = true;
+            for (uint32_t r = 0; r < ny_read; r++) stay &= (YP->yt[r].flags & YT_WRITE) != 0;
+            y.fast = (opt_young_idle != 0 && (y.sparse_rd || !ny_read) && stay) ? 1u : 0u;
+            y.work = d_ywork;
+            idle_ticks += y.fast;
+            skip_ticks += y.sparse_rd;
             y.slot_nt = opt_young_nt ? 1u : 0u;
             y.list = d_ylist;
             // (k_pull_young leaves kListReserve entries of the capacity to k_births' appends)
@@ -2212,6 +2391,10 @@ int gossip_engine::tick_step_a(int64_t t) {
                 HIP_TRY(hipEventRecord(y0, ys));
             }
             last_young_grid = yg;
+            if (y.fast) {  // the idle nodes first (young_kernel.h, k_young_idle)
+                const uint64_t nch = ((uint64_t)(v1 - v0) + 63) / 64;
+                k_young_idle<<<(uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nch + 3) / 4, 16384)), 256, 0, ys>>>(y);
+            }
             k_pull_young<<<yg, 256, young_lds_bytes(ny, ny_read), ys>>>(y);
             HIP_TRY(hipGetLastError());
             if (cfg.flags & GOSSIP_F_TIMING) {
@@ -2391,6 +2574,7 @@ int gossip_engine::tick_step_a(int64_t t) {
     if (young) {  // F_next's slots hold this tick's write-sparse tiles: next tick reads them
         tile_widx.swap(new_widx);
         wt_last.assign(YP->wt, YP->wt + nwt);
+        skip_wr_last = skip_wr && ny && wact;  // (stamped only if this tick launched the young kernel)
     }
     if (smask_any) {  // hop-batched snapshots: arrivals of this tick that precede each snapshot
         const uint64_t cells = (uint64_t)(v1 - v0) * hw;
@@ -2403,6 +2587,7 @@ int gossip_engine::tick_step_a(int64_t t) {
         }
     }
     ft_valid = fused_tick;  // FT[nxt] / d_snz[(t + 1) % 3] describe the next tick's F_cur
+    if (pushw_any && wact) mark_tick = t;  // (d_mark[t & 1] holds this tick's marks)
     return GOSSIP_OK;
 }
 
@@ -3048,6 +3233,9 @@ int gossip_engine_create(const gossip_config* cfg, gossip_engine** out) {
         e->opt_pull_tiles = env_option("GOSSIP_PULL_TILES", 1);
         e->opt_pull_tile_order = env_option("GOSSIP_PULL_TILE_ORDER", 1);
         e->opt_young_nt = env_option("GOSSIP_YOUNG_NT", 1);
+        e->opt_young_skip = env_option("GOSSIP_YOUNG_SKIP", -1);
+        e->opt_pull_push = env_option("GOSSIP_PULL_PUSH", -1);
+        e->opt_young_idle = env_option("GOSSIP_YOUNG_IDLE", 1);
         e->opt_mem_limit = env_option("GOSSIP_MEM_LIMIT", 0);
         e->opt_xchunks = env_option("GOSSIP_XCHUNKS", 4);
         e->opt_late_age = env_option("GOSSIP_LATE_AGE", -1);
@@ -3400,6 +3588,15 @@ int gossip_engine_set_option(gossip_engine* e, const char* name, int64_t value) 
     } else if (k == "young_nt") {
         if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "young_nt: 0 or 1");
         e->opt_young_nt = value;
+    } else if (k == "young_idle") {
+        if (value < 0 || value > 1) return set_error(GOSSIP_EINVAL, "young_idle: 0 or 1");
+        e->opt_young_idle = value;
+    } else if (k == "pull_push") {
+        if (value < -1 || value > 1) return set_error(GOSSIP_EINVAL, "pull_push: -1 (auto), 0 or 1");
+        e->opt_pull_push = value;
+    } else if (k == "young_skip") {
+        if (value < -1 || value > 1) return set_error(GOSSIP_EINVAL, "young_skip: -1 (auto), 0 or 1");
+        e->opt_young_skip = value;
     } else if (k == "young_grid") {
         if (value < 0 || value > (1 << 20)) return set_error(GOSSIP_EINVAL, "young_grid: 0 .. 2^20 blocks");
         e->opt_young_grid = value;
@@ -3443,7 +3640,7 @@ int gossip_engine_get_option(const gossip_engine* e, const char* name, int64_t* 
         {"pull_tile_order", e->opt_pull_tile_order}, {"pull_tiles", e->opt_pull_tiles},
         {"pull_sat", e->opt_pull_sat}, {"dense_rows", e->opt_dense_rows}, {"pull_gate", e->opt_pull_gate},
         {"young_list_cap", e->opt_young_list_cap}, {"young_nt", e->opt_young_nt},
-        {"young_grid", e->opt_young_grid}, {"mem_limit", e->opt_mem_limit}, {"late_age", e->opt_late_age},
+        {"young_skip", e->opt_young_skip}, {"pull_push", e->opt_pull_push}, {"young_idle", e->opt_young_idle}, {"young_grid", e->opt_young_grid}, {"mem_limit", e->opt_mem_limit}, {"late_age", e->opt_late_age},
         {"xchunks", e->opt_xchunks}, {"rehearse_rows", e->opt_rehearse_rows},
         {"dense_fused", e->opt_dense_fused}, {"dense_min_tiles", e->opt_dense_min_tiles}};
     for (const auto& o : opts)
@@ -3844,7 +4041,8 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     // writes (16 B each), row_ptr and the per-node counters.
     c->pull_bytes_moved = 16ull * acct[0] + 4ull * acct[1] + 16ull * (acct[2] + acct[3] + acct[4]) +
                           8ull * acct[7] + e->pull_launches * (8ull * (e->n + 1) + 16ull * e->n + 8ull * e->n * e->ntw) +
-                          16ull * e->n * std::min<uint32_t>(2u, e->ntw) * e->sat_launches;  // sat words r + w
+                          16ull * e->n * std::min<uint32_t>(2u, e->ntw) * e->sat_launches +  // sat words r + w
+                          8ull * acct[32] + (((uint64_t)e->n + 63) / 64 * 8) * e->mark_launches;  // push marks set / read
     c->pull_pair_edges = acct[0];
     c->dense_ops = acct[5];  // k_dense_gemm adds 2*M*N*K of every tile-split it computes
     c->dense_tiles_skipped = acct[6];
@@ -3922,6 +4120,11 @@ int gossip_engine_get_counters(gossip_engine* e, gossip_counters* c) {
     c->pull_gather_items = acct[21];
     c->dense_fused_launches = e->fused_launches;
     c->young_grid = e->last_young_grid;
+    c->young_skip_ticks = (uint32_t)e->skip_ticks;
+    c->young_idle_ticks = e->idle_ticks;
+    c->pull_push_tiles = e->push_tiles;
+    c->pull_pushw_tiles = e->pushw_tiles;
+    c->pull_marks = acct[32];
     c->pull_sat = e->sat_used ? 1u : 0u;
     c->window_early_retires = e->early_retires;
     uint64_t g = 0;
@@ -3976,6 +4179,11 @@ int gossip_engine_reset_timing(gossip_engine* e) {
     e->timers_young.clear();
     e->young_ms_done = 0.0;
     e->young_launches = 0;
+    e->skip_ticks = 0;
+    e->idle_ticks = 0;
+    e->push_tiles = 0;
+    e->pushw_tiles = 0;
+    e->mark_launches = 0;
     e->sat_launches = 0;
     for (auto& p : e->timers_phase) {
         e->event_pool.push_back(p.first);

@@ -43,6 +43,13 @@
 //                 (`sat`, written whole per occupancy word like nz_next) and skips the tile at
 //                 that node -- no own-seen read, no peer row, no occupancy word -- while the host
 //                 trusts the bit (tmask: listed last tick, no birth since, not re-allocated);
+//   push marks -- (round 6, option pull_push) direction-optimising BFS's top-down step for tiles
+//                 whose frontier sits on few nodes (the previous generation's stragglers, a
+//                 tile's first hops): the tick before, every node that writes a non-empty row of
+//                 such a tile (TM_PUSHW) sets its peers' bits in a per-node mark bitmap, and this
+//                 tick the tile (TM_PUSH) is skipped at every UNMARKED node as if saturated -- none
+//                 of its peers holds a row of it, so nothing can arrive.  The sat bits of TM_PUSH
+//                 tiles are written back as 0 (an unmarked node's skip says nothing about them);
 //   dense rows -- (round 4, option dense_rows) tiles whose frontier rows are dense everywhere
 //                 (C4: F_cur at hops 5-7, ~100-760 bits per 1,024-share row) are read WITHOUT
 //                 occupancy words: their writer of the last tick wrote every node's row (WF_DW,
@@ -104,9 +111,11 @@ __device__ __forceinline__ uint32_t group_add(uint32_t x, uint32_t lane) {
 //        read it without occupancy words: dense rows, above)
 enum : uint32_t { WF_CLEAR = 1u, WF_GROUP = 2u, WF_KEEP = 4u, WF_SNAP = 8u, WF_YOUNG = 16u, WF_LATE = 32u,
                   WF_DW = 64u, WF_BIRTH = 128u };  // WF_BIRTH: a generation lands in the word this tick (k_dense_fused)
-// PullArgs::tmask, per occupancy word tw: [3 tw] dense-row tiles (read without occupancy words),
-// [3 tw + 1] tiles whose sat bits are trusted this tick, [3 tw + 2] listed tiles that need occupancy
-enum : uint32_t { TM_DENSE = 0, TM_SATOK = 1, TM_NZ = 2, TM_WORDS = 3 };
+// PullArgs::tmask, per occupancy word tw: [5 tw] dense-row tiles (read without occupancy words),
+// [5 tw + 1] tiles whose sat bits are trusted this tick, [5 tw + 2] listed tiles that need occupancy,
+// [5 tw + 3] push tiles (skipped at unmarked nodes), [5 tw + 4] push-write tiles (rows mark peers)
+enum : uint32_t { TM_DENSE = 0, TM_SATOK = 1, TM_NZ = 2, TM_PUSH = 3, TM_PUSHW = 4, TM_WORDS = 5 };
+constexpr uint32_t kTmSlots = 16;  // LDS words for the launch's (<= 2) occupancy words of tmask
 
 constexpr uint32_t kPullLdsWords = 2048;  // words per launch: LDS liveness, new liveness, flags
 #ifndef PULL_INFLIGHT
@@ -150,8 +159,10 @@ __host__ __device__ constexpr size_t pull_lds_bytes(uint32_t wact, bool keep = f
 // 64 nodes (2 per node), the passes' live-tile masks and forced passes, every wave's per-step pass
 // masks (empty items skipped), behind the rest
 constexpr uint32_t kPullMaxPasses = 32;  // passes of a listed launch: kPullLdsWords / 16 / 4 tiles
-constexpr size_t kPullSatLds = 8u * 8u + 4u * 64u * 2u * 8u + kPullMaxPasses * 8u + 16u + 4u * kPullMaxPasses * 4u;
-static_assert(2u * TM_WORDS <= 8u, "tmask words of a launch fit their LDS slot");
+constexpr size_t kPullSatLds = kTmSlots * 8u + 4u * 64u * 2u * 8u + kPullMaxPasses * 8u + 16u + 4u * kPullMaxPasses * 4u + 4u * 8u;
+// + (push marks) every wave's forced push bits of its 64 nodes (2 occupancy words each)
+constexpr size_t kPullPushLds = 4u * 64u * 2u * 8u;
+static_assert(2u * TM_WORDS <= kTmSlots, "tmask words of a launch fit their LDS slot");
 constexpr uint32_t kNoWord = 0xffffffffu;
 
 // Peer ids of the first GRP peers of item k's node (0xffffffff past the list).
@@ -172,8 +183,10 @@ __device__ __forceinline__ uint32_t pull_cid_load(const PullArgs& a, uint32_t st
 // empty-item skipping and the own-seen gate all on and no diagnostic no-skip -- compile-time
 // flags instead of runtime ones (each runtime flag held a 64-bit SGPR mask; the kernel spilled
 // SGPRs into VGPR lanes, and every reload in the item loop is a VALU instruction)
-template <int LPW, int EPN, bool NT = false, bool SP = false>
+// PUSH (SP only): push marks on (PullArgs::mark_cur / mark_next; engine.hip launch_pull_t)
+template <int LPW, int EPN, bool NT = false, bool SP = false, bool PUSH = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP ? 5 : 1))) void k_pull(PullArgs a) {
+    static_assert(SP || !PUSH, "push marks run in the SP instantiation");
     const bool noskip = SP ? false : a.noskip != 0u;
     constexpr int GRP = LPW * EPN;  // lanes per node
     constexpr int NPW = 64 / GRP;   // nodes per wave step
@@ -198,10 +211,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP ? 5 : 1)
     const bool sat_on = SP || (tm_on && a.sat != nullptr);
     unsigned long long* s_tm = reinterpret_cast<unsigned long long*>(
         reinterpret_cast<char*>(smem) + pull_lds_bytes(a.wact, a.keep_lds != 0, a.nptile));
-    unsigned long long* s_sat = s_tm + 8;  // [wave][node of the chunk][occupancy word of the launch]
+    unsigned long long* s_sat = s_tm + kTmSlots;  // [wave][node of the chunk][occupancy word of the launch]
     unsigned long long* s_plm = s_sat + 4u * 128u;  // [pass] live tiles (bits by tile in its nz word)
     uint32_t* s_pforce = reinterpret_cast<uint32_t*>(s_plm + kPullMaxPasses);  // passes every node runs
     uint32_t* s_smask = s_pforce + 4;  // [wave][step] passes some node of the step has work in
+    // [wave] nodes of the chunk whose rows of push-write tiles mark their peers (push marks)
+    unsigned long long* s_mkw = reinterpret_cast<unsigned long long*>(s_smask + 4u * kPullMaxPasses) + wave_in_block();
+    if (PUSH && (threadIdx.x & 63u) == 0u) *s_mkw = 0ull;
+    // [wave][node][occupancy word]: push tiles an unmarked node skips that its trusted sat bits did
+    // not already cover -- removed from the sat words written back (the skip says nothing about
+    // them; a trusted bit stays true: the node receives nothing in a push tile, live columns only die)
+    unsigned long long* s_psk = s_mkw - wave_in_block() + 4u + (uint64_t)wave_in_block() * 128u;
     if (threadIdx.x < 2u * TM_WORDS) {
         const uint32_t twg = (a.wbase >> 10) + threadIdx.x / TM_WORDS;
         s_tm[threadIdx.x] = (tm_on && twg < a.ntw) ? a.tmask[twg * TM_WORDS + threadIdx.x % TM_WORDS] : 0ull;
@@ -209,15 +229,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP ? 5 : 1)
     // Empty items (tile lists with tmask): an item (node, pass) whose every tile is saturated at
     // the node (a trusted sat bit) or dead (no live column) moves nothing and changes nothing, so
     // the item sequence skips it.  Passes holding a tile that must be written or cleared anyway
-    // (WF_CLEAR, WF_DW, WF_KEEP) and the last pass of each occupancy word (the node's nz and sat
-    // words are written back there, its counters after the last pass) are never skipped.
+    // (WF_CLEAR, WF_DW, WF_KEEP) are never skipped, and a node with any item runs the last pass of
+    // each occupancy word (its nz and sat words are written back there, its counters after the
+    // last pass).  A node with no item at all (round 6: on the sparse ticks of an 8-shard rank,
+    // ~95 % of the nodes) runs none: its sat words are written back before the items.
     constexpr uint32_t TPP_ = LPW >= 8 ? (uint32_t)LPW / 8u : 1u;
     const bool skip_on = SP || (tm_on && a.nptile / TPP_ <= kPullMaxPasses);
     __syncthreads();  // (s_lp, s_wf, s_pt written)
     if (skip_on && threadIdx.x < 64u) {
         const uint32_t p = threadIdx.x, np = a.nptile / TPP_;
         unsigned long long lm = 0ull;
-        bool force = p + 1u == np;
+        bool force = false, last = p + 1u == np;
         if (p < np) {
             for (uint32_t k = 0; k < TPP_; k++) {
                 const uint32_t t = s_pt[p * TPP_ + k];
@@ -233,11 +255,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP ? 5 : 1)
             }
             if (p + 1u < np && ((a.wbase + (uint32_t)s_pt[(p + 1u) * TPP_] * 16u) >> 10) !=
                                    ((a.wbase + (uint32_t)s_pt[p * TPP_] * 16u) >> 10))
-                force = true;
+                last = true;
             s_plm[p] = lm;
         }
-        const unsigned long long fm = __ballot(p < np && force);
-        if (threadIdx.x == 0) s_pforce[0] = (uint32_t)fm;
+        const unsigned long long fm = __ballot(p < np && force), lmk = __ballot(p < np && last);
+        // the launch's occupancy words that hold a pass (bit q: tw_base + q)
+        const unsigned long long tq = __ballot(p < np && ((a.wbase + (uint32_t)s_pt[p * TPP_] * 16u) >> 10) != (a.wbase >> 10));
+        const unsigned long long t0 = __ballot(p < np && ((a.wbase + (uint32_t)s_pt[p * TPP_] * 16u) >> 10) == (a.wbase >> 10));
+        if (threadIdx.x == 0) {
+            s_pforce[0] = (uint32_t)fm;   // passes every node runs
+            s_pforce[1] = (uint32_t)lmk;  // the last pass of each occupancy word (nodes with items)
+            s_pforce[2] = (t0 ? 1u : 0u) | (tq ? 2u : 0u);
+        }
     }
     __syncthreads();
     const uint32_t lane_id = threadIdx.x & 63u;
@@ -282,6 +311,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP ? 5 : 1)
     unsigned long long snap_local = 0ull;
     uint32_t t_pe = 0, t_col = 0, t_srd = 0, t_swr = 0, t_fwr = 0, t_nz = 0, t_sk = 0;  // wave-uniform
     uint32_t t_it = 0, t_gi = 0;  // node items, node items that gathered
+    uint32_t t_mk = 0;            // push marks set (one 8-B atomic each)
     unsigned long long nzacc = 0ull;
     const bool gather = EPN == 1;  // the pipelined id/occupancy loads
     const uint32_t tw_base = a.wbase >> 10;  // the launch's first occupancy word
@@ -301,24 +331,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP ? 5 : 1)
         const int64_t rp = a.rowptr[min(c0 + lane, n)];
         const int64_t rp_end = a.rowptr[min(c0 + 64u, n)];
         if (sat_on) {  // the chunk's sat words, trusted bits only (waited for below)
+            const uint64_t vj = c0 + lane;
+            // push tiles are skipped at an unmarked node like saturated ones (header comment)
+            const bool unmarked = PUSH && a.mark_cur && vj < n && !((a.mark_cur[vj >> 6] >> (vj & 63u)) & 1ull);
 #pragma unroll
             for (uint32_t q = 0; q < 2u; q++) {
-                const uint64_t vj = c0 + lane;
                 const uint32_t twg = tw_base + q;
-                s_satw[lane * 2u + q] = (vj < n && twg < a.ntw)
-                                            ? a.sat[vj * a.ntw + twg] & s_tm[q * TM_WORDS + TM_SATOK] : 0ull;
+                const unsigned long long tr = (vj < n && twg < a.ntw) ? a.sat[vj * a.ntw + twg] & s_tm[q * TM_WORDS + TM_SATOK] : 0ull;
+                const unsigned long long pk = (unmarked && vj < n && twg < a.ntw) ? s_tm[q * TM_WORDS + TM_PUSH] & ~tr : 0ull;
+                s_satw[lane * 2u + q] = tr | pk;
+                if (PUSH) s_psk[lane * 2u + q] = pk;
             }
         }
         // per step, the passes some node of the step has work in (skip_on; else every pass)
         uint32_t* s_sm = s_smask + wave_in_block() * kPullMaxPasses;
         if (skip_on) {
-            uint32_t m = s_pforce[0];
+            uint32_t m = 0u;
             const uint64_t vj = c0 + lane;
             if (vj < n) {
                 for (uint32_t p = 0; p < npass; p++) {
                     const uint32_t twp = tw_of(p) - tw_base;
                     // (s_satw: this lane's node, written above by this lane)
                     if ((s_plm[p] & ~(sat_on ? s_satw[lane * 2u + twp] : 0ull)) != 0ull) m |= 1u << p;
+                }
+                m |= s_pforce[0];
+                if (m || !PUSH) {  // (the idle-node skip runs in the PUSH instantiation only)
+                    m |= s_pforce[1];
+                } else if (sat_on) {  // no item: the node's sat words now (nz_next was zeroed)
+                    const uint32_t tq = s_pforce[2];
+#pragma unroll
+                    for (uint32_t q = 0; q < 2u; q++)
+                        if ((tq >> q) & 1u)
+                            a.sat[vj * a.ntw + tw_base + q] = s_satw[lane * 2u + q] & ~(PUSH ? s_psk[lane * 2u + q] : 0ull);
                 }
             }
             m = group_or<NPW>(m, lane);  // (the NPW nodes of a step are adjacent lanes)
@@ -338,28 +382,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP ? 5 : 1)
                 ps1 = (uint32_t)__builtin_ctz(m);
             } else {
                 st1 = st + 1u;
+                if constexpr (PUSH)
+                    while (st1 < nsteps && s_sm[st1] == 0u) st1++;  // (steps without an item)
                 ps1 = st1 < nsteps ? (uint32_t)__builtin_ctz(s_sm[st1]) : 0u;
             }
         };
         // item k = (step, pass): node c0 + step * NPW + slot, the lane's word pair lw_of(pass)
-        uint32_t step = 0, pass = skip_on ? (uint32_t)__builtin_ctz(s_sm[0]) : 0u;
+        uint32_t step = 0, pass = 0u;
+        if (skip_on) {
+            if constexpr (PUSH)
+                while (step < nsteps && s_sm[step] == 0u) step++;
+            pass = step < nsteps ? (uint32_t)__builtin_ctz(s_sm[step]) : 0u;
+        }
         uint32_t first_step = 0xffffffffu;  // the step whose peer range beg/end holds
         ulonglong2 s2c = make_ulonglong2(0ull, 0ull);
-        {
-            const uint64_t v = c0 + slot;
+        if (step < nsteps) {
+            const uint64_t v = c0 + step * NPW + slot;
             const uint32_t lw = lw_of(pass, wl);
             if (v < n && lw != kNoWord && (s_lp[lw] | s_lp[lw + 1u]) != 0ull &&
-                !((satv_of(slot, tw_of(pass)) >> (((a.wbase + lw) >> 4) & 63u)) & 1ull))
+                !((satv_of(step * NPW + slot, tw_of(pass)) >> (((a.wbase + lw) >> 4) & 63u)) & 1ull))
                 s2c = load_row16<NT>(a.seen + v * stride + a.wbase + lw);
         }
         uint32_t cid0 = 0xffffffffu, cid1 = 0xffffffffu;
         unsigned long long nz0 = 0ull;
-        if (gather) {
+        if (gather && step < nsteps) {
             uint32_t s1, p1;
-            next_item(0u, pass, s1, p1);
-            cid0 = pull_cid_load<LPW, EPN>(a, 0u, c0, rp, rp_end, gl, slot);
-            cid1 = s1 == 0u ? cid0 : pull_cid_load<LPW, EPN>(a, s1, c0, rp, rp_end, gl, slot);
-            const bool ld = cid0 != 0xffffffffu && nz_needed(slot, tw_of(pass));
+            next_item(step, pass, s1, p1);
+            cid0 = pull_cid_load<LPW, EPN>(a, step, c0, rp, rp_end, gl, slot);
+            cid1 = s1 == step ? cid0 : s1 < nsteps ? pull_cid_load<LPW, EPN>(a, s1, c0, rp, rp_end, gl, slot) : 0xffffffffu;
+            const bool ld = cid0 != 0xffffffffu && nz_needed(step * NPW + slot, tw_of(pass));
             nz0 = ld ? a.nz_cur[(uint64_t)cid0 * a.ntw + tw_of(pass)] : 0ull;
             t_nz += wave_count(ld);
         }
@@ -603,6 +654,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP ? 5 : 1)
             ta = (int)group_or<8>((uint32_t)ta, lane);
             // a WF_DW tile's row is written at every node (zeros too): read as a dense row next tick
             const bool trow = ta || (act && (f0 & WF_DW));
+            // ---- push marks: a non-empty row of a push-write tile marks every peer of the node,
+            //      after the chunk's items (the node's bit in the wave's LDS word meanwhile) ----
+            if (PUSH && a.mark_next && ta && act && (wl & 7u) == 0u &&
+                ((s_tm[(tw - tw_base) * TM_WORDS + TM_PUSHW] & tbit) != 0ull))
+                atomicOr(s_mkw, 1ull << idx);
             // ---- saturation bit of the tile: every live column of it seen, after this tick ----
             // (want = live & unseen & kept, so want & ~new are the live columns still unseen; a
             // keep-masked word's dropped columns are unseen too: never saturated on a keep tick)
@@ -658,7 +714,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP ? 5 : 1)
                             a.nz_next[(uint64_t)v * a.ntw + tw] = nzacc;
                         else if (nzacc)
                             atomicOr(&a.nz_next[(uint64_t)v * a.ntw + tw], nzacc);
-                        if (sat_on) a.sat[(uint64_t)v * a.ntw + tw] = s_satw[idx * 2u + (tw - tw_base)];
+                        if (sat_on)
+                            a.sat[(uint64_t)v * a.ntw + tw] = s_satw[idx * 2u + (tw - tw_base)] &
+                                                              ~(PUSH ? s_psk[idx * 2u + (tw - tw_base)] : 0ull);
                     }
                     nzacc = 0ull;
                 }
@@ -683,16 +741,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SP ? 5 : 1)
             step = step1;
             pass = pass1;
         }
+        if (PUSH && a.mark_next) {  // (uniform) the chunk's marking nodes: every peer's bit (rare by the
+            __builtin_amdgcn_wave_barrier();  //  host's choice of push-write tiles)
+            unsigned long long mk = *s_mkw;
+            __builtin_amdgcn_wave_barrier();
+            if (lane_id == 0) *s_mkw = 0ull;
+            uint32_t nm = 0;
+            while (mk) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(mk);
+                mk &= mk - 1ull;
+                const int32_t b = (int32_t)lane_read((uint32_t)rp, j);
+                const int32_t e = j + 1u < 64u ? (int32_t)lane_read((uint32_t)rp, j + 1u) : (int32_t)rp_end;
+                for (int32_t q = b + (int32_t)lane_id; q < e; q += 64) {
+                    const uint32_t u = (uint32_t)a.col[q];
+                    atomicOr(&a.mark_next[u >> 6], 1ull << (u & 63u));
+                    nm++;
+                }
+            }
+            t_mk += wave_sum32(nm);
+        }
     }
     if (a.snap) {
         snap_local = wave_sum(snap_local);
         if (lane_id == 0 && snap_local) atomicAdd(a.snap, snap_local);
     }
     if (a.acct && lane_id == 0) {
-        const uint32_t tv[9] = {t_pe, t_col, t_srd, t_swr, t_fwr, t_nz, t_sk, t_it, t_gi};
-        const int slot_of[9] = {0, 1, 2, 3, 4, 7, 16, 20, 21};
+        const uint32_t tv[10] = {t_pe, t_col, t_srd, t_swr, t_fwr, t_nz, t_sk, t_it, t_gi, t_mk};
+        const int slot_of[10] = {0, 1, 2, 3, 4, 7, 16, 20, 21, 32};
 #pragma unroll
-        for (int q = 0; q < 9; q++)
+        for (int q = 0; q < 10; q++)
             if (tv[q]) acct_add(a.acct, (uint32_t)slot_of[q], (unsigned long long)tv[q]);
     }
     __syncthreads();

@@ -109,6 +109,24 @@ struct YoungArgs {
     uint8_t* hint_next;
     const int32_t* rev;
     uint32_t stamp_cur, stamp_next;
+    // Empty-slot skipping (round 6, option young_skip).  On the ticks after a shard's births most
+    // slots are EMPTY (C4, one rank of 8: the births tick's slots hold ~34k of 10M nodes' entries,
+    // the next tick's ~5 %), yet every node read its ~16 peers' slot lines -- 25 GB per launch for
+    // nothing.  When the host expects the slots written this tick to be sparse (sparse_wr), every
+    // writer of a NON-EMPTY slot (here and in k_births) also stamps its reverse entries, with
+    // stamp1_next for one line (stamp_next still means two lines), and the next tick's readers
+    // (sparse_rd) load only the peers whose hint byte carries one of the two stamps: an unstamped
+    // peer's slot is empty (a stale byte that happens to match costs one useless line, never a
+    // result).  The hint bytes ride with the peer ids, so skipping adds no round trip.
+    uint32_t stamp1_cur, stamp1_next;
+    uint32_t sparse_rd, sparse_wr;
+    // Idle nodes (round 6): with nothing to read but stamped slots (sparse_rd, or no read tile) and
+    // no young tile leaving or gone (every seen-list entry stays), a node none of whose peers holds
+    // a stamped slot gets no bit and keeps its list: per 64-node chunk, one pass over the chunk's
+    // hint bytes finds the nodes with work, and the others only get an empty slot and their list
+    // header's this-tick part folded into `kept` -- no per-node walk (~800 VALU each).
+    uint32_t fast;
+    unsigned long long* work;  // fast: per 64-node chunk from v0, its nodes with work (k_young_idle)
     uint32_t slot_nt;  // option young_nt: non-temporal slot-line loads (C4 shard, young alone 21.1 -> 19.0 ms)
     uint16_t* list;        // n x kListU16 seen lists
     const uint8_t* ymap;   // [64] young id -> position in yt (0xff: none)
@@ -249,13 +267,33 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             return (uint32_t)a.col[b + (int32_t)lane];
         };
         auto with_hint = [&](uint32_t id, uint32_t hint) -> uint32_t {
-            return (id != 0xffffffffu && hint == a.stamp_cur) ? id | 0x80000000u : id;
+            if (id == 0xffffffffu) return id;
+            if (hint == a.stamp_cur) return id | 0x80000000u;
+            return (a.sparse_rd && hint != a.stamp1_cur) ? 0xffffffffu : id;  // (an empty slot: skipped)
         };
+        // sparse_rd: the peers left after with_hint, moved to the front of the wave (lane p = the
+        // p-th peer with a stamped slot), so the gather's batches cover them only (np0 = their number)
+        auto compact = [&](uint32_t id, uint32_t lane) -> uint32_t {
+            const unsigned long long m = __ballot(id != 0xffffffffu);
+            uint32_t* sc = reinterpret_cast<uint32_t*>(s_out);  // (free until the node's dedup)
+            if (id != 0xffffffffu) sc[lanes_below(m)] = id;
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t r = lane < (uint32_t)__popcll(m) ? sc[lane] : 0xffffffffu;
+            __builtin_amdgcn_wave_barrier();
+            return r;
+        };
+        // the chunk's nodes with work: every node, unless k_young_idle found the idle ones (fast)
+        const unsigned long long work = a.fast ? a.work[(c0 - a.v0) >> 6]
+                                               : cnt_nodes >= 64u ? ~0ull : ((1ull << cnt_nodes) - 1ull);
         uint32_t h_cur = 0u;
         int32_t rv_cur = -1;
-        uint32_t cid_cur = load_ids(0u, h_cur, rv_cur);
+        uint32_t jn = work ? (uint32_t)__builtin_ctzll(work) : 64u;
+        uint32_t cid_cur = load_ids(jn, h_cur, rv_cur);
         cid_cur = with_hint(cid_cur, h_cur);
-        for (uint32_t jn = 0; jn < cnt_nodes; jn++) {
+        for (; jn < cnt_nodes;) {
+            // the next node with work (64: none)
+            const unsigned long long wn = jn + 1u < 64u ? work & ~((2ull << jn) - 1ull) : 0ull;
+            const uint32_t jnext = wn ? (uint32_t)__builtin_ctzll(wn) : 64u;
             const uint32_t lane = opaque(lane_id);
             const uint64_t v = c0 + jn;
             // the 8 entries of a lane's 16-B piece of a slot line; `hdr`: entry 0 is the line's header
@@ -352,7 +390,13 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
                     t_fb += a.nr;
                 }
             };
-            const int32_t np0 = min(64, end - beg);
+            // (sparse_rd: only the stamped peers, compacted; nr == 0 -- no read tile, e.g. a births
+            //  tick after a tick without young tiles -- nothing to gather at all)
+            if (a.nr == 0u)
+                cid_cur = 0xffffffffu;
+            else if (a.sparse_rd)
+                cid_cur = compact(cid_cur, lane);
+            const int32_t np0 = a.nr == 0u ? 0 : a.sparse_rd ? (int32_t)wave_count(cid_cur != 0xffffffffu) : min(64, end - beg);
             t_col += (uint32_t)max(0, end - beg);
             unsigned long long ovf = 0ull;
             YDUP(7) issue(cid_cur, 0);
@@ -361,7 +405,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             t_lr += 2u;
             uint32_t h_next = 0u;
             int32_t rv_next = -1;
-            const uint32_t cid_next = load_ids(jn + 1u, h_next, rv_next);  // the next node's peers
+            const uint32_t cid_next = load_ids(jnext, h_next, rv_next);  // the next node's peers
             YSTAMP(0);
             YDUP(1) consume(cid_cur, 0, np0, ovf);
             for (int32_t pb = 8 * kYoungQ; pb < np0; pb += 8 * kYoungQ) {  // degree > 8 kYoungQ
@@ -369,13 +413,10 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
                 consume(cid_cur, pb, np0, ovf);
             }
             fallback(cid_cur, ovf);
-            for (int32_t cb = beg + 64; cb < end; cb += 64) {  // peers beyond the first 64 (rare)
+            for (int32_t cb = beg + 64; a.nr && cb < end; cb += 64) {  // peers beyond the first 64 (rare)
                 const int32_t np = min(64, end - cb);
                 uint32_t cid = 0xffffffffu;
-                if ((int32_t)lane < np) {
-                    cid = (uint32_t)a.col[cb + (int32_t)lane];
-                    if (a.hint_cur[cb + (int32_t)lane] == a.stamp_cur) cid |= 0x80000000u;
-                }
+                if ((int32_t)lane < np) cid = with_hint((uint32_t)a.col[cb + (int32_t)lane], a.hint_cur[cb + (int32_t)lane]);
                 unsigned long long ovf2 = 0ull;
                 for (int32_t pb = 0; pb < np; pb += 8 * kYoungQ) {
                     issue(cid, pb);
@@ -535,11 +576,14 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
                 if (lane < 8u * lines)
                     *reinterpret_cast<ulonglong2*>(out + lane * 8u) = *reinterpret_cast<const ulonglong2*>(s_out + lane * 8u);
                 t_slw += lines;
-                if (lines == 2u) {  // announce the second line to the readers of the next tick
-                    if (rv >= 0) a.hint_next[rv] = (uint8_t)a.stamp_next;  // (the first 64 peers)
+                // announce a second line to the readers of the next tick -- and, sparse_wr, any
+                // non-empty slot (an overflowed one too: its readers must see the header)
+                if (lines == 2u || (a.sparse_wr && slot_total > 0u)) {
+                    const uint8_t hv = (uint8_t)(lines == 2u ? a.stamp_next : a.stamp1_next);
+                    if (rv >= 0) a.hint_next[rv] = hv;  // (the first 64 peers)
                     for (int32_t j = beg + 64 + (int32_t)lane; j < end; j += 64) {
                         const int32_t r = a.rev[j];
-                        if (r >= 0) a.hint_next[r] = (uint8_t)a.stamp_next;
+                        if (r >= 0) a.hint_next[r] = hv;
                     }
                 }
             }
@@ -633,6 +677,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             const uint32_t c = wave_sum32(cnt);
             if (lane == 0 && c) atomicAdd(&a.recv[v], c);  // no-return: nothing waits (sent: derived)
             YSTAMP(7);
+            jn = jnext;
         }
     }
     if (a.snap) {
@@ -649,5 +694,68 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
 #pragma unroll
         for (int q = 0; q < 11; q++)
             if (tv[q]) acct_add(a.acct, slot_of[q], (unsigned long long)tv[q]);
+    }
+}
+
+// The idle-node pass of a `fast` tick (YoungArgs::fast), one lane per node, before k_pull_young on
+// its stream: a node with work has a peer whose slot is stamped (its entries' hint bytes, 4 at a
+// time) or an overflowed seen list while fresh tiles need clearing (k_pull_young's walk does that);
+// every other node gets an empty slot and its list header's this-tick part folded into `kept`
+// (k_births tests id groups against entries [1, kept] only).  Writes each chunk's work mask.
+__global__ __launch_bounds__(256) void k_young_idle(YoungArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nchunks = ((uint64_t)a.n - a.v0 + 63u) / 64u;
+    uint32_t t_lw = 0, t_idle = 0;
+    for (uint64_t ch = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6); ch < nchunks; ch += (uint64_t)gridDim.x * 4u) {
+        const uint64_t c0 = a.v0 + ch * 64u;
+        const uint32_t cnt_nodes = (uint32_t)min<uint64_t>(64u, a.n - c0);
+        const uint64_t v = c0 + lane;
+        bool w = false;
+        uint32_t lh = kListOverflow;
+        if (lane < cnt_nodes) {
+            if (a.nr) {  // some peer's slot is stamped (the hint bytes of this node's entries)
+                const int32_t b = (int32_t)a.rowptr[v], e = (int32_t)a.rowptr[v + 1];
+                const uint32_t p1 = a.stamp1_cur * 0x01010101u, p2 = a.stamp_cur * 0x01010101u;
+                for (int32_t q = b & ~3; q < e; q += 4) {
+                    const uint32_t x = *reinterpret_cast<const uint32_t*>(a.hint_cur + q);
+                    uint32_t valid = 0xffffffffu;  // (the bytes inside [b, e))
+                    if (q < b) valid <<= 8 * (b - q);
+                    if (q + 4 > e) valid &= 0xffffffffu >> (8 * (q + 4 - e));
+                    // a zero byte of x ^ stamp, by the borrow test (a false hit is only work)
+                    const uint32_t z1 = x ^ p1, z2 = x ^ p2;
+                    if ((((z1 - 0x01010101u) & ~z1) | ((z2 - 0x01010101u) & ~z2)) & 0x80808080u & valid) {
+                        w = true;
+                        break;
+                    }
+                }
+            }
+            lh = a.list[v * kListU16];
+            if (lh == kListOverflow && a.ny > a.nr) w = true;  // (its fresh tiles' seen words)
+        }
+        const unsigned long long work = __ballot(w);
+        if (lane == 0) a.work[ch] = work;
+        if (lane < cnt_nodes && !w && lh != kListOverflow && (lh >> 7) != (lh & 127u)) {
+            a.list[v * kListU16] = (uint16_t)list_header(lh & 127u, lh & 127u);
+            t_lw++;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < 8u; i++) {
+            const uint32_t j = i * 8u + (lane >> 3);
+            if (j < cnt_nodes && !((work >> j) & 1ull)) {
+                ulonglong2 x = make_ulonglong2(~0ull, ~0ull);  // tombstones
+                if ((lane & 7u) == 0u) x.x = ~0ull << 16;      // (entry 0: the header, 0)
+                *reinterpret_cast<ulonglong2*>(a.slot_next + (c0 + j) * kSlotU16 + (lane & 7u) * 8u) = x;
+            }
+        }
+        t_idle += cnt_nodes - (uint32_t)__popcll(work);
+    }
+    // idle nodes' slot lines written and header lines read (acct 14, 17), headers rewritten (18)
+    const uint32_t lw = wave_sum32(t_lw);
+    if (a.acct && lane == 0) {
+        if (t_idle) {
+            acct_add(a.acct, 14u, (unsigned long long)t_idle);
+            acct_add(a.acct, 17u, (unsigned long long)t_idle);
+        }
+        if (lw) acct_add(a.acct, 18u, (unsigned long long)lw);
     }
 }

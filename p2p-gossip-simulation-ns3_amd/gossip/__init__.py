@@ -115,7 +115,9 @@ class gossip_counters(C.Structure):
         ("window_early_retires", C.c_uint64), ("young_list_lines", C.c_uint64),
         ("pull_items", C.c_uint64), ("pull_gather_items", C.c_uint64),
         ("dense_fused_launches", C.c_uint64),
-        ("young_grid", C.c_uint32), ("pad1", C.c_uint32),
+        ("young_grid", C.c_uint32), ("young_skip_ticks", C.c_uint32),
+        ("pull_push_tiles", C.c_uint64), ("pull_pushw_tiles", C.c_uint64), ("pull_marks", C.c_uint64),
+        ("young_idle_ticks", C.c_uint64),
     ]
 
 

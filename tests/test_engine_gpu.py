@@ -352,3 +352,45 @@ def test_parity_65536_sparse(gossip, oracle):
     assert np.array_equal(node[ek], tn[ok]) and np.array_equal(sid[ek], ti[ok])
     assert np.array_equal(tick[ek], tt[ok] // L) and np.array_equal(hop[ek], th[ok])
     assert int(st.recv.sum()) > n  # the floods covered the graph
+
+
+# Push marks (round 6, option pull_push, pull_kernel.h): rows of push-write tiles mark their
+# writers' peers, and the next tick's k_pull skips push tiles at unmarked nodes.  Forced on every
+# listed tile that is not dense-row (1) -- so tiles at every hop, with births landing in old tiles
+# (collisions: packed tiles), keep masks (the in-tick cut of an odd latency) and young tiles beside
+# -- the counters and traces must equal the oracle's; auto (-1) picks the tiles by the layer model.
+PUSH = {"forced": {"pull_push": 1}, "forced_young": {"pull_push": 1, "young": 1},
+        "forced_dense_rows": {"pull_push": 1, "dense_rows": 1}, "forced_nt": {"pull_push": 1, "pull_nt": 1},
+        "auto": {"pull_push": -1}, "off": {"pull_push": 0}}
+
+
+@pytest.mark.parametrize("case", ["wide_collisions", "odd_latency_cut", "packed_tiles"])
+@pytest.mark.parametrize("opts", list(PUSH))
+def test_push_marks(gossip, oracle, case, opts):
+    n, deg, seed, sim, lat_ms, id_mask, fl = {
+        "wide_collisions": (3000, 8.0, 45, 6.3, 5.0, 0xFFF, gossip.F_TILE_PER_TICK),
+        "odd_latency_cut": (3000, 8.0, 27, 6.37, 2.3, 0, gossip.F_TILE_PER_TICK),
+        "packed_tiles": (4096, 16.0, 21, 6.0, 5.0, 0x3FFF, 0)}[case]
+    topo = gossip.Topology.gnp(n, deg / (n - 1), seed, gossip.TOPO_SKIP)
+    lat = gossip.milliseconds_to_ns(lat_ms)
+    t_cut = gossip.seconds_to_ns(sim - 0.1)
+    ev = gossip.make_schedule(n, seed + 1, T0, t_cut, id_mask=id_mask)
+    eng = _engine_for(gossip, topo, ev, lat, t_cut, flags=gossip.F_TRACE | fl, options=tuple(PUSH[opts].items()))
+    st, c = eng.stats(), eng.counters()
+    a, b = topo.links()
+    r = oracle.run_replay(n, lat, T0, t_cut, a, b, ev["ns"], ev["node"], ev["share_id"], trace=True)
+    for k in STATS:
+        assert np.array_equal(getattr(st, k), getattr(r, k)), k
+    node, sid, tick, hop, via = eng.trace()
+    tn, ti, tt, th, tv = r.trace
+    ek, ok = np.lexsort((sid, node)), np.lexsort((ti, tn))
+    assert np.array_equal(node[ek], tn[ok]) and np.array_equal(sid[ek], ti[ok])
+    assert np.array_equal(tick[ek], tt[ok] // lat) and np.array_equal(hop[ek], th[ok])
+    assert np.array_equal(via[ek], tv[ok])
+    if opts == "off":
+        assert c.pull_push_tiles == 0 and c.pull_marks == 0
+    elif opts in ("forced", "forced_young", "forced_nt") and c.pull_lpw == 32:
+        # (push marks run in k_pull<32, 1, .., SP>; with dense rows forced every tile but the
+        # freshest is dense-row, and a fresh tile got births the tick before: never a push tile)
+        assert c.pull_pushw_tiles > 0 and c.pull_push_tiles > 0 and c.pull_marks > 0, c.pull_lpw
+    eng.close()

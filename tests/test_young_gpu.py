@@ -194,3 +194,56 @@ def test_young_off_equals_on(gossip, overlap, nt):
         assert np.array_equal(getattr(a, k), getattr(b, k)), k
     on.close()
     off.close()
+
+
+# Empty-slot skipping (round 6, option young_skip, young_kernel.h): writers of non-empty slots stamp
+# their peers' hint bytes, and the next tick's readers load only stamped peers' slot lines.  Forced on
+# every tick (1) it must still equal the oracle through overflowed slots (cap 1: headers read through
+# the stamp), two-line slots (cap 64 on a dense graph, > 64 peers per node), k_births' first entries
+# (a birth into an empty slot stamps it) and id groups; 0 turns it off; auto (-1) fires on the sparse
+# ticks of these small graphs (births and their first hop).
+@pytest.mark.parametrize("case", ["overflow", "groups", "dense", "shared", "off", "auto"])
+def test_young_empty_slot_skipping(gossip, oracle, case):
+    tpt = gossip.F_TILE_PER_TICK
+    if case == "overflow":
+        c = _parity(gossip, oracle, 4096, 16.0 / 4095, 71, 6.0, 5.0, dict(young_cap=1, young_age=3, young_skip=1), flags=tpt)
+        assert c.young_fallback_rows > 0
+    elif case == "groups":
+        c = _parity(gossip, oracle, 400, 0.01, 73, 15.0, 5.0, dict(young_cap=2, young_age=4, young_skip=1),
+                    id_mask=0x3FF, flags=tpt)
+    elif case == "dense":
+        c = _parity(gossip, oracle, 700, 0.3, 76, 5.6, 5.0, dict(young_cap=64, young_age=2, young_skip=1), flags=tpt)
+    elif case == "shared":
+        c = _parity(gossip, oracle, 600, 0.008, 74, 12.0, 5.0, dict(young_cap=4, young_age=5, young_skip=1), id_mask=0x7FF)
+    elif case == "off":
+        c = _parity(gossip, oracle, 4096, 16.0 / 4095, 71, 6.0, 5.0, dict(young_age=5, young_skip=0), flags=tpt)
+        assert c.young_skip_ticks == 0
+        return
+    else:
+        c = _parity(gossip, oracle, 4096, 16.0 / 4095, 71, 6.0, 5.0, dict(young_age=5, young_skip=-1), flags=tpt)
+        assert 0 < c.young_skip_ticks < c.young_launches
+        return
+    assert c.young_skip_ticks > 0 and c.young_launches > 0
+
+
+# The idle-node pass (round 6, option young_idle, k_young_idle): on a tick whose k_pull_young reads
+# only stamped slots and keeps every seen list, nodes without a stamped peer skip the node walk --
+# an empty slot and the list header's kept part written by the pass instead.  With id groups (births
+# testing their group against the list's kept entries), overflowing lists (fresh tiles cleared by the
+# walk) and young tiles of every age, on and off must both equal the oracle.
+@pytest.mark.parametrize("case", ["plain", "groups", "list_overflow", "off"])
+def test_young_idle_nodes(gossip, oracle, case):
+    tpt = gossip.F_TILE_PER_TICK
+    if case == "plain":
+        c = _parity(gossip, oracle, 4096, 16.0 / 4095, 71, 6.0, 5.0, dict(young_age=5, young_skip=1), flags=tpt)
+    elif case == "groups":
+        c = _parity(gossip, oracle, 400, 0.01, 73, 15.0, 5.0, dict(young_cap=3, young_age=5, young_skip=1),
+                    id_mask=0x3FF, flags=tpt)
+    elif case == "list_overflow":
+        c = _parity(gossip, oracle, 400, 0.01, 73, 15.0, 5.0, dict(young_cap=8, young_age=4, young_list_cap=4, young_skip=1),
+                    id_mask=0x3FF, flags=tpt)
+    else:
+        c = _parity(gossip, oracle, 4096, 16.0 / 4095, 71, 6.0, 5.0, dict(young_age=5, young_skip=1, young_idle=0), flags=tpt)
+        assert c.young_idle_ticks == 0
+        return
+    assert c.young_idle_ticks > 0
