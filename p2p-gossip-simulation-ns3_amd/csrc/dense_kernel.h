@@ -439,6 +439,7 @@ constexpr uint32_t kFMiscOff = kFIncOff + kDenseTile * 4u * 8u;
 constexpr uint32_t kFActWords = 4;                          // active-tile bits: windows <= 4,096 words
 constexpr uint32_t kFActOff = kFMiscOff + 64u;
 constexpr uint32_t kFMaxCt = kFActWords * 64u * 4u;         // column tiles of the widest window
+static_assert(kFMaxCt <= 4096u, "the prefix scan packs a live-tile count of 12 bits");
 constexpr uint32_t kFCtOff = kFActOff + kFActWords * 8u;    // per column tile: units, prefix (u32)
 constexpr uint32_t kFLctOff = kFCtOff + 2u * kFMaxCt * 4u;  // the column tiles with units, in order (u16)
 constexpr uint32_t kFFlgOff = kFLctOff + kFMaxCt * 2u;      // per column tile: its 4 word-flag bytes
@@ -649,7 +650,8 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
     auto active = [&](uint32_t ct) -> bool { return (sAct[ct >> 8] >> ((ct >> 2) & 63u)) & 1ull; };
     // exclusive prefix over the column tiles of (units << 12 | live), so the same scan places the
     // live column tiles: each thread sums a run of them, the block scans the runs (units < 2^20:
-    // nt <= 2,048 column tiles x <= 512 stages)
+    // the host's gate ntw <= kFActWords keeps nt <= kFMaxCt = 1,024 column tiles -- the LDS
+    // tables' size, and what keeps the packed 12-bit live count exact -- x <= 512 stages)
     const uint32_t run = (a.nt + 511u) / 512u, c0 = t * run;
     uint32_t mine = 0;
     for (uint32_t c = c0; c < min(a.nt, c0 + run); c++) mine += (sCtU[c] << 12) | (sCtU[c] ? 1u : 0u);
@@ -1044,11 +1046,14 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
             unsigned long long* ip = a.inc + vlo * a.stride + w0 + wn;
             if (lo && vlo < a.n) atomicOr(ip, (unsigned long long)lo);
             if (hi && vlo + 64u < a.n) atomicOr(ip + 64ull * a.stride, (unsigned long long)hi);
-            __syncthreads();  // (every wave's atomics done: vmcnt(0) before the barrier)
+            // release: every wave's atomics are performed before its barrier, so none
+            // lands after the completing block's exchange (a barrier alone need not wait for them)
+            __threadfence();
+            __syncthreads();
             if (t == 0) {
                 const uint32_t mineu = (uint32_t)(end - seg_b);  // units this block reduced into the tile
                 const uint32_t T = mblk * a.nt + ct;
-                const uint32_t old = __hip_atomic_fetch_add(&a.tix[T], mineu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t old = __hip_atomic_fetch_add(&a.tix[T], mineu, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
                 const bool last = old + mineu == sCtU[ct];
                 if (last) __hip_atomic_store(&a.tix[T], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 sMisc[5] = last ? 1ull : 0ull;
@@ -1056,6 +1061,7 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
             __syncthreads();
             DSTAMP(4);
             if (sMisc[5]) {
+                __threadfence();  // (acquire: the other blocks' released atomics come first)
                 // (atomic exchange: the other blocks' atomics are read where they were performed)
                 if (ev < a.n) {
                     unsigned long long* rp = a.inc + ev * a.stride + wa;

@@ -39,6 +39,7 @@
 #include <numeric>
 #include <queue>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <type_traits>
 #include <unordered_map>
@@ -57,6 +58,8 @@ namespace {
             return set_error(GOSSIP_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
 
+// gossip_engine_abort: seconds to wait for a collective being enqueued before aborting anyway
+constexpr int kAbortWaitS = 10;
 // A collective being enqueued on an engine's communicator (COMM_TRY, gossip_engine_abort)
 struct CommIssue {
     std::atomic<int>& c;
@@ -2395,7 +2398,10 @@ int gossip_engine::tick_step_a(int64_t t) {
                 const uint64_t nch = ((uint64_t)(v1 - v0) + 63) / 64;
                 k_young_idle<<<(uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nch + 3) / 4, 16384)), 256, 0, ys>>>(y);
             }
-            k_pull_young<<<yg, 256, young_lds_bytes(ny, ny_read), ys>>>(y);
+            if (y.sparse_rd || y.fast || !ny_read)
+                k_pull_young<true><<<yg, 256, young_lds_bytes(ny, ny_read), ys>>>(y);
+            else
+                k_pull_young<false><<<yg, 256, young_lds_bytes(ny, ny_read), ys>>>(y);
             HIP_TRY(hipGetLastError());
             if (cfg.flags & GOSSIP_F_TIMING) {
                 HIP_TRY(hipEventRecord(y1, ys));
@@ -2482,6 +2488,8 @@ int gossip_engine::tick_step_a(int64_t t) {
             f.n = n; f.n_pad = n_pad; f.kw = n_pad / 32u; f.stride = stride;
             f.nst = n_pad / kStageK; f.nstw = snz_nstw;
             f.mb = n_pad / kDenseTile; f.nt = wact / 4u; f.total = f.mb * f.nt;
+            if (f.nt > kFMaxCt)  // (fused_tick's ntw gate implies it: the kernel's LDS tables hold kFMaxCt)
+                return set_error(GOSSIP_EHIP, "k_dense_fused: window wider than its column-tile tables");
             f.wact = wact;
             f.inc = d_inc;
             f.tix = d_tix;
@@ -2727,7 +2735,9 @@ DevLayout dev_layout(uint64_t k, uint32_t ntw, uint32_t wlive) {
 // memory -- the engine then reports GOSSIP_ESTATE.  The issue is bracketed by comm_issuing, and
 // gossip_engine_abort raises `aborted` first and then waits for comm_issuing == 0 before it frees
 // the communicator (both sequentially consistent): a call that saw `aborted` clear finishes
-// enqueueing before the abort, a later one sees it set.  (Enqueueing never waits for the peers.)
+// enqueueing before the abort, a later one sees it set -- unless the enqueue blocks on a failed
+// peer for kAbortWaitS, when the abort goes ahead to unblock it.  A grouped exchange takes one
+// bracket for its whole ncclGroupStart .. ncclGroupEnd (exchange_rccl).
 // CommIssue is defined at the top of the file.
 #define COMM_TRY(x)                                                                         \
     do {                                                                                    \
@@ -3023,18 +3033,28 @@ int gossip_engine::exchange_rccl(int64_t t) {
         HIP_TRY(hipStreamWaitEvent(xstream, ev_chunk[c], 0));
         if ((rc = pack_dev(t, lo, hi, wl, xstream))) return rc;
         COMM_TRY(ncclAllGather(d_msg, d_tot + (size_t)c * R, 1, ncclUint64, comm, xstream));
-        COMM_TRY(ncclGroupStart());
-        for (uint32_t r = 0; r < R; r++) {
-            uint64_t rlo, rhi;
-            uint32_t rwl;
-            geom(r, c, &rlo, &rhi, &rwl);
-            const uint64_t words = dev_layout(rhi - rlo, ntw, rwl).rows + 16ull * xcap[(size_t)r * kMaxChunks + c];
-            uint64_t* buf = r == row_rank ? d_msg : d_recv_msgs + at[(size_t)c * R + r];
-            COMM_TRY(ncclBroadcast(buf, buf, words, ncclUint64, (int)r, comm, xstream));
-            if (r == row_rank) exchange_bytes_out += words * 8;
-            else exchange_bytes_in += words * 8;
+        {
+            // ONE issue bracket around the whole group: `aborted` is tested once,
+            // before ncclGroupStart, and the group is always closed -- an early return between
+            // ncclGroupStart and ncclGroupEnd would leave this thread's RCCL group open, holding
+            // broadcasts on a communicator the abort then frees
+            CommIssue issuing_(comm_issuing);
+            if (aborted.load()) return set_error(GOSSIP_ESTATE, "RCCL: the row partition was aborted");
+            ncclResult_t gr = ncclGroupStart();
+            for (uint32_t r = 0; r < R && gr == ncclSuccess; r++) {
+                uint64_t rlo, rhi;
+                uint32_t rwl;
+                geom(r, c, &rlo, &rhi, &rwl);
+                const uint64_t words = dev_layout(rhi - rlo, ntw, rwl).rows + 16ull * xcap[(size_t)r * kMaxChunks + c];
+                uint64_t* buf = r == row_rank ? d_msg : d_recv_msgs + at[(size_t)c * R + r];
+                gr = ncclBroadcast(buf, buf, words, ncclUint64, (int)r, comm, xstream);
+                if (r == row_rank) exchange_bytes_out += words * 8;
+                else exchange_bytes_in += words * 8;
+            }
+            const ncclResult_t ge = ncclGroupEnd();
+            if (gr != ncclSuccess || ge != ncclSuccess)
+                return set_error(GOSSIP_EHIP, std::string("RCCL: ") + ncclGetErrorString(gr != ncclSuccess ? gr : ge));
         }
-        COMM_TRY(ncclGroupEnd());
         for (uint32_t r = 0; r < R; r++) {
             if (r == row_rank) continue;
             uint64_t rlo, rhi;
@@ -3416,9 +3436,13 @@ int gossip_engine_abort(gossip_engine* e) {
     if (!e) return set_error(GOSSIP_EINVAL, "NULL engine");
     bool expected = false;
     // the flag first: the engine's own thread checks it before every collective (COMM_TRY); then
-    // wait until no collective is being enqueued on the communicator, and free it
+    // wait until no collective is being enqueued on the communicator, and free it.  The wait has a
+    // deadline: an issue can block inside RCCL on a peer that already failed (lazy
+    // connection setup on the first collective), and unblocking exactly that is ncclCommAbort's job
     if (e->aborted.compare_exchange_strong(expected, true) && e->comm) {
-        while (e->comm_issuing.load() != 0) std::this_thread::yield();
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(kAbortWaitS);
+        while (e->comm_issuing.load() != 0 && std::chrono::steady_clock::now() < deadline)
+            std::this_thread::yield();
         ncclCommAbort(e->comm);
     }
     return GOSSIP_OK;

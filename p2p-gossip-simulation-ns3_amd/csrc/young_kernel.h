@@ -210,6 +210,10 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
 #ifndef YOUNG_MIN_WAVES
 #define YOUNG_MIN_WAVES 4
 #endif
+// SPARSE: the instantiation of the sparse ticks (engine.hip launch_young: empty-slot skipping, the
+// idle-node pass's work masks, no read tile); the other one keeps the dense ticks' register
+// allocation (SGPR spills 54 vs 72: ~0.5 ms per C4 shard-tick, profiles/r06/)
+template <bool SPARSE>
 __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a) {
     extern __shared__ unsigned long long smem[];
     const uint32_t nrw = a.nr * 16u;  // accumulated words
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
         auto with_hint = [&](uint32_t id, uint32_t hint) -> uint32_t {
             if (id == 0xffffffffu) return id;
             if (hint == a.stamp_cur) return id | 0x80000000u;
-            return (a.sparse_rd && hint != a.stamp1_cur) ? 0xffffffffu : id;  // (an empty slot: skipped)
+            return (SPARSE && a.sparse_rd && hint != a.stamp1_cur) ? 0xffffffffu : id;  // (an empty slot: skipped)
         };
         // sparse_rd: the peers left after with_hint, moved to the front of the wave (lane p = the
         // p-th peer with a stamped slot), so the gather's batches cover them only (np0 = their number)
@@ -283,17 +287,17 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             return r;
         };
         // the chunk's nodes with work: every node, unless k_young_idle found the idle ones (fast)
-        const unsigned long long work = a.fast ? a.work[(c0 - a.v0) >> 6]
-                                               : cnt_nodes >= 64u ? ~0ull : ((1ull << cnt_nodes) - 1ull);
+        const unsigned long long work = (SPARSE && a.fast) ? a.work[(c0 - a.v0) >> 6]
+                                                           : cnt_nodes >= 64u ? ~0ull : ((1ull << cnt_nodes) - 1ull);
         uint32_t h_cur = 0u;
         int32_t rv_cur = -1;
-        uint32_t jn = work ? (uint32_t)__builtin_ctzll(work) : 64u;
+        uint32_t jn = SPARSE ? (work ? (uint32_t)__builtin_ctzll(work) : 64u) : 0u;
         uint32_t cid_cur = load_ids(jn, h_cur, rv_cur);
         cid_cur = with_hint(cid_cur, h_cur);
         for (; jn < cnt_nodes;) {
             // the next node with work (64: none)
-            const unsigned long long wn = jn + 1u < 64u ? work & ~((2ull << jn) - 1ull) : 0ull;
-            const uint32_t jnext = wn ? (uint32_t)__builtin_ctzll(wn) : 64u;
+            const unsigned long long wn = (SPARSE && jn + 1u < 64u) ? work & ~((2ull << jn) - 1ull) : 0ull;
+            const uint32_t jnext = !SPARSE ? jn + 1u : wn ? (uint32_t)__builtin_ctzll(wn) : 64u;
             const uint32_t lane = opaque(lane_id);
             const uint64_t v = c0 + jn;
             // the 8 entries of a lane's 16-B piece of a slot line; `hdr`: entry 0 is the line's header
@@ -392,11 +396,12 @@ __global__ __launch_bounds__(256, YOUNG_MIN_WAVES) void k_pull_young(YoungArgs a
             };
             // (sparse_rd: only the stamped peers, compacted; nr == 0 -- no read tile, e.g. a births
             //  tick after a tick without young tiles -- nothing to gather at all)
-            if (a.nr == 0u)
+            if (SPARSE && a.nr == 0u)
                 cid_cur = 0xffffffffu;
-            else if (a.sparse_rd)
+            else if (SPARSE && a.sparse_rd)
                 cid_cur = compact(cid_cur, lane);
-            const int32_t np0 = a.nr == 0u ? 0 : a.sparse_rd ? (int32_t)wave_count(cid_cur != 0xffffffffu) : min(64, end - beg);
+            const int32_t np0 = !SPARSE ? min(64, end - beg)
+                                : a.nr == 0u ? 0 : a.sparse_rd ? (int32_t)wave_count(cid_cur != 0xffffffffu) : min(64, end - beg);
             t_col += (uint32_t)max(0, end - beg);
             unsigned long long ovf = 0ull;
             YDUP(7) issue(cid_cur, 0);

@@ -190,6 +190,22 @@ static void topology_and_schedule() {
     std::vector<uint32_t> owner(m);
     CHECK("shard rule", gossip_shard_events(t, m, ev.data(), 3, owner.data()) == GOSSIP_OK);
     for (uint32_t w : owner) CHECK("shard range", w < 3);
+    // the birth-tick rule, its collision branch too: ids folded to 6 bits collide
+    // across nodes, and every (id, component) instance must stay on one shard
+    {
+        std::vector<gossip_gen_event> cev(ev.begin(), ev.end());
+        for (auto& x : cev) x.share_id &= 0x3fu;
+        std::vector<uint32_t> own8(m);
+        CHECK("shard by tick", gossip_shard_events_by_tick(t, m, cev.data(), 8, L, own8.data()) == GOSSIP_OK);
+        bool whole = true;
+        for (uint64_t i = 0; i < m; i++) {
+            CHECK("shard by tick range", own8[i] < 8);
+            for (uint64_t j = i + 1; j < m; j++)  // (n = 60 is one component: same id, same shard)
+                if (cev[i].share_id == cev[j].share_id && own8[i] != own8[j]) whole = false;
+        }
+        CHECK("shard by tick keeps instances whole", whole);
+        CHECK("shard by tick bad latency", gossip_shard_events_by_tick(t, m, cev.data(), 8, 0, own8.data()) != GOSSIP_OK);
+    }
 
     // the report (p2pnetwork.cc:253-285) with full and truncated buffers
     const int64_t rl = gossip_format_statistics(n, gen.data(), recv.data(), fwd.data(), sent.data(), proc.data(),

@@ -175,6 +175,20 @@ def test_c4_sample_matches_oracle_a(gossip, oracle, c4):
     tot = _sum(parts)
     for k in SUM_STATS:
         assert np.array_equal(tot[k], getattr(ref, k).astype(np.uint64)), ("2 shards", k)
+    # the 8-GPU layout's rule (bench.shard_flags): 8 shards by birth tick, a fresh tile per birth
+    # tick -- an id instance stays whole on the shard of its first generation (G1-G5 above: later
+    # generations of an instance in its old tile) -- with young tiles, empty-slot skipping and the
+    # idle-node pass forced (the sample is too thin for their auto rules)
+    tick = gossip.F_SHARD_BY_TICK | gossip.F_TILE_PER_TICK
+    for opts in ((), (("young", 1), ("young_skip", 1), ("young_cap", 8))):
+        runs8 = [_run(gossip, topo, ev, W.T0_NS, t_cut, options=opts, max_words=16, shard_rank=r, shard_count=8,
+                      flags=tick) for r in range(8)]
+        tot = _sum([st for st, _ in runs8])
+        for k in SUM_STATS:
+            assert np.array_equal(tot[k], getattr(ref, k).astype(np.uint64)), ("8 shards by birth tick", opts, k)
+        assert sum(c.edge_events for _, c in runs8) == ref.edge_events
+        if opts:
+            assert sum(c.young_skip_ticks for _, c in runs8) > 0 and sum(c.young_idle_ticks for _, c in runs8) > 0
 
 
 def _c4_headline_sample(gossip, c4, per_tick=20, ticks=24):
@@ -230,11 +244,26 @@ def test_c4_headline_kernels_match_oracle_b(gossip, oracle, c4):
         assert c.pull_tiles == 1 and c.pull_late_age == 1 and c.young_launches > 0, name
         if dict(opts).get("pull_sat", 1):
             assert c.pull_sat == 1 and c.pull_sat_skips > 0, name
+    # the same kernels as the 8 ranks of the 8-GPU layout run them (bench.shard_flags: birth-tick
+    # rule, a fresh tile per birth tick), every sparse-tick path forced: empty-slot skipping and the
+    # idle-node pass in k_pull_young, push marks in k_pull and k_births (pull_push 1: every listed
+    # tile; a shard's window here is <= 3 tiles, so its k_pull is the narrow one -- the production
+    # k_pull<32,1,..,PUSH> at C4 scale is test_c4_tick_rule_slice_equals_continuous_run's)
+    tick = gossip.F_SHARD_BY_TICK | gossip.F_TILE_PER_TICK
+    sparse = prod + (("young_skip", 1), ("pull_push", 1))
+    runs8 = [_run(gossip, topo, ev, W.T0_NS, t_cut, options=sparse, flags=tick, shard_rank=r, shard_count=8)
+             for r in range(8)]
+    tot = _sum([st for st, _ in runs8])
+    for k in SUM_STATS:
+        assert np.array_equal(tot[k], getattr(ref, k).astype(np.uint64)), ("8 shards by birth tick", k)
+    assert sum(c.edge_events for _, c in runs8) == ref.edge_events
+    assert sum(c.young_skip_ticks for _, c in runs8) > 0 and sum(c.young_idle_ticks for _, c in runs8) > 0
 
 
-def _c4_shard_deltas(gossip, topo, ev, shard, shards, t0, t1, options=()):
+def _c4_shard_deltas(gossip, topo, ev, shard, shards, t0, t1, options=(), flags=0):
     W = _w()
-    eng = gossip.Engine(topo.num_nodes, W.L_NS, W.T0_NS, W.T_CUT_NS, shard_rank=shard, shard_count=shards)
+    eng = gossip.Engine(topo.num_nodes, W.L_NS, W.T0_NS, W.T_CUT_NS, shard_rank=shard, shard_count=shards,
+                        flags=flags)
     for k, v in options:
         eng.set_option(k, v)
     eng.set_topology(topo)
@@ -296,6 +325,43 @@ def test_c4_bench_slice_equals_continuous_run(gossip, c4):
     assert ca1.words_hw > 200 and int(a1.recv.sum()) > 100 * len(gens)
     # the bench's pull: young-tile slots, the early exit on every tile
     assert ca1.young_launches > 0 and ca1.pull_late_age == 1
+
+
+def test_c4_tick_rule_slice_equals_continuous_run(gossip, c4):
+    # The 8-GPU layout's own rank (bench.shard_flags at 8 shards: birth-tick rule, a fresh tile per
+    # birth tick, young tiles and every sparse-tick path on auto -- empty-slot skipping, the
+    # idle-node pass, push marks in the production k_pull<32,1,true,SP,PUSH>): shard 1 of 8 of the
+    # bench's warm-start slice against the continuous run from t = 5 s of the same shard, per-node
+    # deltas of the timed ticks bit-identical (the slice is exact iff every older flood has died out,
+    # DESIGN.md section 4), and both against the reference's counter invariants.
+    W = _w()
+    topo = c4[0]
+    n = topo.num_nodes
+    warm, steps = 5, 20
+    t0 = W.SLICE_NS // W.L_NS + warm
+    t1 = t0 + steps
+    ev_s, _ = W.slice_schedule(n, W.CONFIGS["C4"]["node_seed"], W.SLICE_NS, t1 * W.L_NS)
+    ev_c = gossip.make_schedule(n, W.CONFIGS["C4"]["node_seed"], W.T0_NS, W.T_CUT_NS, t_gen_end_ns=t1 * W.L_NS,
+                                threads=16)
+    shards, shard = 8, 1
+    own_s = gossip.shard_events(topo, ev_s, shards, by_tick_latency_ns=W.L_NS)
+    tick = gossip.F_SHARD_BY_TICK | gossip.F_TILE_PER_TICK
+    a0, a1, ca0, ca1 = _c4_shard_deltas(gossip, topo, ev_s, shard, shards, t0, t1, flags=tick)
+    b0, b1, cb0, cb1 = _c4_shard_deltas(gossip, topo, ev_c, shard, shards, t0, t1, flags=tick)
+    for k in ("recv", "gen", "sent", "processed"):
+        da = getattr(a1, k).astype(np.int64) - getattr(a0, k).astype(np.int64)
+        db = getattr(b1, k).astype(np.int64) - getattr(b0, k).astype(np.int64)
+        assert np.array_equal(da, db), (k, int(np.count_nonzero(da != db)))
+    assert ca1.edge_events - ca0.edge_events == cb1.edge_events - cb0.edge_events > 0
+    _invariants(a1, ca1)
+    _invariants(b1, cb1)
+    mine = ev_s[own_s == shard]
+    gens = mine[mine["ns"] < t1 * W.L_NS]
+    assert int(a1.gen.sum()) == len(gens) == ca1.generations
+    # the sparse-tick paths ran in the timed ticks (counters restart at reset_timing: c1 - c0 here
+    # is cumulative since creation, so check the slice run's totals)
+    assert ca1.young_skip_ticks > 0 and ca1.young_idle_ticks > 0, "empty-slot skipping / idle pass"
+    assert ca1.pull_push_tiles > 0 and ca1.pull_marks > 0 and ca1.pull_lpw == 32, "push marks"
 
 
 # ------------------------------------------------------------------------------------------- C5

@@ -4,7 +4,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd $R
-timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py -k "push or sharded" -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/r6f_tests.log 2>&1 || { tail -30 gpurun_out/r6f_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py -k "push or sharded" tests/test_dense_fused_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/r6f_tests.log 2>&1 || { tail -30 gpurun_out/r6f_tests.log; exit 1; }
 tail -1 gpurun_out/r6f_tests.log
 L=$R/p2p-gossip-simulation-ns3_amd/lib
 run() {  # name lib args...
