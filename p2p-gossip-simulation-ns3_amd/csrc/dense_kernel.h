@@ -431,6 +431,11 @@ struct FusedArgs {
     uint32_t rmax;                         // most data-parallel rounds (A/B: GOSSIP_DENSE_ROUNDS)
     uint32_t gm;                           // row blocks per tile group (tile order, header comment)
     unsigned long long* pts;               // nullable: [4] block 0's start, [5] max block end (phase timer)
+    // Row partition (round 6, engine.hip fused_rows): the launch covers the rows of row blocks
+    // [mb0, mb0 + mb) -- the host offsets every per-row pointer (Ab, seen, Fnext, recv, inc,
+    // nz_next) and FTn by the first row and sets n to the rank's row count; only the stage bit of a
+    // tile's F_next (a 1,024-node stage of the WHOLE node range) needs the absolute row block.
+    uint32_t mb0;
 };
 
 constexpr uint32_t kFStageBytes = 2u * kDenseTile * 128u;  // A + B rows of one 1024-k stage
@@ -870,7 +875,7 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
             const unsigned long long x = sMisc[t];
             if (x) atomicOr(&a.live[w0 + t], x);  // (no return: nothing waits for it)
         } else if (t == 4u && sMisc[4]) {
-            const uint32_t stg = mblk >> 2;  // 4 row blocks of 256 per 1024-k stage
+            const uint32_t stg = (a.mb0 + mblk) >> 2;  // 4 row blocks of 256 per 1024-k stage
             atomicOr(&a.snz_n[(uint64_t)ct * a.nstw + (stg >> 6)], 1ull << (stg & 63u));
         }
         __syncthreads();  // (sInc / sMisc reuse by the next tile)
@@ -1118,6 +1123,55 @@ __global__ __launch_bounds__(512, 1) void k_dense_fused(FusedArgs a) {
             uint32_t z = 0;
             for (uint32_t c = 0; c < a.nt; c++) z += sCtU[c] == 0u;
             if (z) acct_add(a.acct, 6, (unsigned long long)z * a.mb);
+        }
+    }
+}
+
+// ---- FT slice exchange (row partition with the fused tick, engine.hip exchange_ft) -----------
+// A rank's message, u32 words: [W x S] its nodes' bits of every window column of FT_next (column c:
+// words [c S, c S + S), the rank's rows lo .. hi as words lo / 32 .. of FT's column row; S = the
+// largest rank's word count, zero-padded), then [2 nsnz] its F_next stage masks, [2 wact] its partial
+// liveness.  Every rank all-gathers the messages and unpacks the others' (k_ft_unpack).
+__global__ __launch_bounds__(256) void k_ft_pack(const uint32_t* __restrict__ FT, uint32_t kw, uint32_t lo_w,
+                                                 uint32_t S, uint32_t Sown, uint32_t W,
+                                                 const unsigned long long* __restrict__ snz, uint32_t nsnz,
+                                                 const unsigned long long* __restrict__ live, uint32_t wact,
+                                                 uint32_t* __restrict__ msg) {
+    const uint64_t nft = (uint64_t)W * S, tot = nft + 2ull * nsnz + 2ull * wact;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < tot; i += (uint64_t)gridDim.x * 256u) {
+        uint32_t x;
+        if (i < nft) {
+            const uint32_t c = (uint32_t)(i / S), j = (uint32_t)(i - (uint64_t)c * S);
+            x = j < Sown ? FT[(uint64_t)c * kw + lo_w + j] : 0u;
+        } else if (i < nft + 2ull * nsnz) {
+            const uint64_t k = i - nft;
+            x = (uint32_t)(snz[k >> 1] >> (32u * (k & 1u)));
+        } else {
+            const uint64_t k = i - nft - 2ull * nsnz;
+            x = (uint32_t)(live[k >> 1] >> (32u * (k & 1u)));
+        }
+        msg[i] = x;
+    }
+}
+// Rank r's message into this rank's FT_next (its rows' words of every column), stage masks and
+// liveness (OR: every rank's stage bits and live words are partial)
+__global__ __launch_bounds__(256) void k_ft_unpack(uint32_t* __restrict__ FT, uint32_t kw, uint32_t lo_w, uint32_t S,
+                                                   uint32_t Sr, uint32_t W, const uint32_t* __restrict__ msg,
+                                                   unsigned long long* __restrict__ snz, uint32_t nsnz,
+                                                   unsigned long long* __restrict__ live, uint32_t wact) {
+    const uint64_t nft = (uint64_t)W * S, tot = nft + nsnz + wact;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < tot; i += (uint64_t)gridDim.x * 256u) {
+        if (i < nft) {
+            const uint32_t c = (uint32_t)(i / S), j = (uint32_t)(i - (uint64_t)c * S);
+            if (j < Sr) FT[(uint64_t)c * kw + lo_w + j] = msg[i];
+        } else {
+            const uint64_t k = i - nft;
+            const uint32_t* p = msg + nft + 2ull * k;
+            const unsigned long long x = (unsigned long long)p[0] | ((unsigned long long)p[1] << 32);
+            if (x) {
+                if (k < nsnz) snz[k] |= x;
+                else live[k - nsnz] |= x;
+            }
         }
     }
 }

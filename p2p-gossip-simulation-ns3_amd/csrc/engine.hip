@@ -767,6 +767,20 @@ struct gossip_engine {
     unsigned long long* d_snz[3] = {nullptr, nullptr, nullptr};
     uint32_t snz_nstw = 0;              // mask words per column tile
     bool ft_valid = false;              // d_FT[fcur] / d_snz[fcur] were written by the fused path
+    // Fused row partition (round 6): every DENSE tick of a row rank runs k_dense_fused over its own
+    // rows and the ranks all-gather FT_next slices (exchange_ft) instead of F_next rows -- with the
+    // RCCL and lockstep (group_run) backends, when the schedule holds no id group (a group word
+    // needs the three-kernel path, whose k_transpose reads every rank's F rows)
+    bool fused_rows = false;
+    bool group_mode = false;            // stepped by gossip_engine_group_run
+    uint32_t* d_ftmsg = nullptr;        // this rank's FT slice message (k_ft_pack)
+    uint32_t* d_ftrecv = nullptr;       // RCCL: every rank's message, all-gathered
+    uint64_t ftmsg_cap = 0, ftrecv_cap = 0;  // (u64 words: ensure_dev)
+    uint64_t ft_words(uint32_t wact) const;  // one rank's message (u32 words) at window wact
+    uint32_t ft_smax() const;                // u32 words of the largest rank's rows
+    int ft_pack(int64_t t);                  // this rank's message of tick t (engine stream)
+    int ft_unpack(int64_t t, uint32_t r, const uint32_t* msg);  // rank r's message into this rank
+    int exchange_ft(int64_t t);
     int64_t opt_dense_fused = 1;        // 1: k_dense_fused when the tick allows it (tick_step_a)
     int64_t dense_rounds = -1;          // k_dense_fused's most data-parallel rounds (A/B env GOSSIP_DENSE_ROUNDS; -1: all)
     int64_t dense_gm = 4;               // k_dense_fused's row blocks per tile group (A/B env GOSSIP_DENSE_GM)
@@ -1008,7 +1022,7 @@ gossip_engine::~gossip_engine() {
     hipFree(d_rowptr); hipFree(d_col); hipFree(d_deg);
     hipFree(d_rowptr_c); hipFree(d_col_c); hipFree(d_degc);
     for (int k = 0; k < 4; k++) { hipFree(d_smask[k]); hipHostFree(h_smask[k]); }
-    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen_mem); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_sat); hipFree(d_mark[0]); hipFree(d_mark[1]); hipFree(d_Ab); hipFree(d_FT[0]); hipFree(d_FT[1]); hipFree(d_snz[0]); hipFree(d_snz[1]); hipFree(d_snz[2]); hipFree(d_tix); hipFree(d_inc);
+    hipFree(d_F[0]); hipFree(d_F[1]); hipFree(d_seen_mem); hipFree(d_nz[0]); hipFree(d_nz[1]); hipFree(d_sat); hipFree(d_mark[0]); hipFree(d_mark[1]); hipFree(d_Ab); hipFree(d_FT[0]); hipFree(d_FT[1]); hipFree(d_snz[0]); hipFree(d_snz[1]); hipFree(d_snz[2]); hipFree(d_tix); hipFree(d_inc); hipFree(d_ftmsg); hipFree(d_ftrecv);
     hipFree(d_recv); hipFree(d_gen); hipFree(d_effgen); hipFree(d_sent); hipFree(d_phase_ts);
     hipFree(d_live[0]); hipFree(d_live[1]); hipFree(d_live[2]); hipFree(d_scalars); hipFree(d_acct);
     hipFree(d_msg); hipFree(d_cnt); hipFree(d_scan_tmp); hipFree(d_recv_msgs); hipFree(d_sizes);
@@ -1563,22 +1577,27 @@ int gossip_engine::grow(uint32_t new_stride) {
         if (!rc) rc = regrow_host(h_live[k], 8, stride, new_stride);
     }
     if (rc) return rc;
-    if (dense) {  // transposed frontier and incoming words: rebuilt (k_transpose next tick), no copy
-        const uint64_t ft = (uint64_t)new_stride * 8 * n_pad;
-        const uint64_t snzb = (uint64_t)(new_stride / 4u) * snz_nstw * 8u;
+    if (dense) {  // transposed frontier: the new columns are appended (column c at c x kw words, its
+                  // stage masks at c / 256 x nstw), so the old ones are copied and stay valid -- a
+                  // fused row partition could not rebuild them (k_transpose reads every rank's F rows)
+        const uint64_t ft = (uint64_t)new_stride * 8 * n_pad, ft_old = (uint64_t)stride * 8 * n_pad;
+        const uint64_t snzb = (uint64_t)(new_stride / 4u) * snz_nstw * 8u, snzb_old = (uint64_t)(stride / 4u) * snz_nstw * 8u;
         for (int k = 0; k < 3; k++) {
             if (k < 2) {
+                uint32_t* q = nullptr;
+                HIP_TRY(hipMalloc(&q, ft));
+                HIP_TRY(hipMemset(q, 0, ft));
+                HIP_TRY(hipMemcpy(q, d_FT[k], ft_old, hipMemcpyDeviceToDevice));
                 HIP_TRY(hipFree(d_FT[k]));
-                d_FT[k] = nullptr;
-                HIP_TRY(hipMalloc(&d_FT[k], ft));
-                HIP_TRY(hipMemset(d_FT[k], 0, ft));
+                d_FT[k] = q;
             }
+            unsigned long long* z = nullptr;
+            HIP_TRY(hipMalloc(&z, snzb));
+            HIP_TRY(hipMemset(z, 0, snzb));
+            HIP_TRY(hipMemcpy(z, d_snz[k], snzb_old, hipMemcpyDeviceToDevice));
             HIP_TRY(hipFree(d_snz[k]));
-            d_snz[k] = nullptr;
-            HIP_TRY(hipMalloc(&d_snz[k], snzb));
-            HIP_TRY(hipMemset(d_snz[k], 0, snzb));
+            d_snz[k] = z;
         }
-        ft_valid = false;
         HIP_TRY(hipFree(d_inc));
         d_inc = nullptr;
         HIP_TRY(hipMalloc(&d_inc, nb));
@@ -1935,7 +1954,9 @@ int gossip_engine::tick_step_a(int64_t t) {
     }
     // 3c. row chunks of the pipelined exchange: births grouped by chunk (a node has at most one
     //     birth per tick, so their order inside a launch is free)
-    nchunks = row_count > 1 ? (uint32_t)std::min<int64_t>(kMaxChunks, std::max<int64_t>(1, opt_xchunks)) : 1u;
+    fused_rows = row_count > 1 && dense && opt_dense_fused && (comm || group_mode) && max_group_phases == 0 &&
+                 !(cfg.flags & GOSSIP_F_NOSKIP);
+    nchunks = (row_count > 1 && !fused_rows) ? (uint32_t)std::min<int64_t>(kMaxChunks, std::max<int64_t>(1, opt_xchunks)) : 1u;
     uint32_t cb_off[kMaxChunks + 1] = {};
     cb_off[1] = nb;
     if (nchunks > 1) {
@@ -2174,9 +2195,11 @@ int gossip_engine::tick_step_a(int64_t t) {
     const int nxt = fcur ^ 1;
     // DENSE ticks run k_dense_fused (dense_kernel.h) unless the tick has id groups, row chunks
     // (row partition: other ranks' rows reach F_next without FT), or the diagnostic no-skip pull
-    const bool fused_tick = dense && wact && opt_dense_fused && nchunks == 1 && row_count == 1 &&
+    const bool fused_tick = dense && wact && opt_dense_fused && nchunks == 1 && (row_count == 1 || fused_rows) &&
                             !(cfg.flags & GOSSIP_F_NOSKIP) && !group_any && ntw <= kFActWords &&
                             (uint64_t)(wact / 4u) * (n_pad / kStageK) < (1ull << 20);  // (its packed unit scan)
+    if (fused_rows && wact && !fused_tick)  // (the other ranks' F rows are not exchanged)
+        return set_error(GOSSIP_ECAPACITY, "fused row partition: the window outgrew the fused kernel (<= 4,096 words)");
     // births [off, off + cnt) of the staged array (all of them, or one row chunk's)
     auto launch_births = [&](uint32_t off, uint32_t cnt) -> int {
         if (!cnt) return GOSSIP_OK;
@@ -2477,21 +2500,26 @@ int gossip_engine::tick_step_a(int64_t t) {
         } else if (fused_tick) {
             // the whole DENSE pull in one persistent kernel (contraction, dedup, FT of F_next)
             FusedArgs f;
-            f.Ab = d_Ab; f.FTc = d_FT[fcur]; f.FTn = d_FT[nxt];
+            // a row rank: its rows [v0, v1) (row blocks of 256 from v0 / 256; v0 is 512-aligned)
+            const uint64_t r0 = row_count > 1 ? v0 : 0u;
+            const uint32_t rows = row_count > 1 ? v1 - v0 : n;
+            f.Ab = d_Ab + r0 * (n_pad / 32u); f.FTc = d_FT[fcur]; f.FTn = d_FT[nxt] + r0 / 32u;
+            f.mb0 = (uint32_t)(r0 / kDenseTile);
             f.snz_c = d_snz[t % 3];  // (by the last tick's fused kernel + births, or k_transpose above)
             f.snz_n = d_snz[(t + 1) % 3];
             f.snz_z = d_snz[(t + 2) % 3];
             f.snz_zwords = (stride / 4u) * snz_nstw;
-            f.seen = d_seen; f.Fnext = d_F[nxt]; f.ctl = d_ctl[slot]; f.wflags = d_wflags[slot];
-            f.recv = d_recv; f.live = d_live[lv]; f.live_prev = a.live_prev; f.snap = snap_ptr; f.acct = d_acct;
-            f.nz_next = d_nz[nxt]; f.ntw = ntw;
-            f.n = n; f.n_pad = n_pad; f.kw = n_pad / 32u; f.stride = stride;
+            f.seen = d_seen + r0 * stride; f.Fnext = d_F[nxt] + r0 * stride; f.ctl = d_ctl[slot]; f.wflags = d_wflags[slot];
+            f.recv = d_recv + r0; f.live = d_live[lv]; f.live_prev = a.live_prev; f.snap = snap_ptr; f.acct = d_acct;
+            f.nz_next = d_nz[nxt] + r0 * ntw; f.ntw = ntw;
+            f.n = rows; f.n_pad = n_pad; f.kw = n_pad / 32u; f.stride = stride;
             f.nst = n_pad / kStageK; f.nstw = snz_nstw;
-            f.mb = n_pad / kDenseTile; f.nt = wact / 4u; f.total = f.mb * f.nt;
+            f.mb = row_count > 1 ? (rows + kDenseTile - 1u) / kDenseTile : n_pad / kDenseTile;
+            f.nt = wact / 4u; f.total = f.mb * f.nt;
             if (f.nt > kFMaxCt)  // (fused_tick's ntw gate implies it: the kernel's LDS tables hold kFMaxCt)
                 return set_error(GOSSIP_EHIP, "k_dense_fused: window wider than its column-tile tables");
             f.wact = wact;
-            f.inc = d_inc;
+            f.inc = d_inc + r0 * stride;
             f.tix = d_tix;
             f.rmax = dense_rounds < 0 ? 0xffffffffu : (uint32_t)dense_rounds;
             f.pts = (pts && ft_valid) ? pts : nullptr;  // (a tick with k_transpose keeps the stamp-kernel span)
@@ -3108,11 +3136,70 @@ int gossip_engine::exchange_rccl(int64_t t) {
     return GOSSIP_OK;
 }
 
+// Fused row partition: one rank's FT slice message (dense_kernel.h k_ft_pack), u32 words
+uint64_t gossip_engine::ft_words(uint32_t wact) const {
+    return (uint64_t)wact * 64u * ft_smax() + 2ull * (wact / 4u) * snz_nstw + 2ull * wact;
+}
+
+// The fused tick's exchange over RCCL: every rank packs its FT_next slice, stage masks and partial
+// liveness, one all-gather (the north star's frontier all-gather: W shares x n bits in total, 32 MiB
+// per hop at C5), and each rank unpacks the others' into its FT_next, stage masks and liveness --
+// on the engine stream, after the tick's births, before the liveness read-back.  F_next rows and
+// occupancy words stay per rank (nothing reads another rank's: the next fused tick reads FT).
+int gossip_engine::ft_pack(int64_t t) {
+    const uint32_t wact = hw;
+    const uint64_t words = ft_words(wact);
+    uint64_t* m = reinterpret_cast<uint64_t*>(d_ftmsg);
+    int rc = ensure_dev(m, ftmsg_cap, (words + 1) / 2);
+    d_ftmsg = reinterpret_cast<uint32_t*>(m);
+    if (rc) return rc;
+    const uint32_t g = (uint32_t)std::min<uint64_t>((words + 255) / 256, 8192);
+    k_ft_pack<<<g, 256, 0, stream>>>(d_FT[fcur ^ 1], n_pad / 32u, row_lo[row_rank] / 32u, ft_smax(),
+                                     (uint32_t)((row_lo[row_rank + 1] - row_lo[row_rank] + 31) / 32), wact * 64u,
+                                     d_snz[(t + 1) % 3], (wact / 4u) * snz_nstw, d_live[t % 3], wact, d_ftmsg);
+    HIP_TRY(hipGetLastError());
+    exchange_bytes_out += words * 4;
+    return GOSSIP_OK;
+}
+int gossip_engine::ft_unpack(int64_t t, uint32_t r, const uint32_t* msg) {
+    const uint32_t wact = hw;
+    const uint64_t words = ft_words(wact);
+    const uint32_t g = (uint32_t)std::min<uint64_t>((words + 255) / 256, 8192);
+    k_ft_unpack<<<g, 256, 0, stream>>>(d_FT[fcur ^ 1], n_pad / 32u, row_lo[r] / 32u, ft_smax(),
+                                       (uint32_t)((row_lo[r + 1] - row_lo[r] + 31) / 32), wact * 64u, msg,
+                                       d_snz[(t + 1) % 3], (wact / 4u) * snz_nstw, d_live[t % 3], wact);
+    HIP_TRY(hipGetLastError());
+    exchange_bytes_in += words * 4;
+    return GOSSIP_OK;
+}
+uint32_t gossip_engine::ft_smax() const {
+    uint64_t smax = 0;
+    for (uint32_t r = 0; r < row_count; r++) smax = std::max<uint64_t>(smax, (row_lo[r + 1] - row_lo[r] + 31) / 32);
+    return (uint32_t)smax;
+}
+int gossip_engine::exchange_ft(int64_t t) {
+    const uint32_t R = row_count;
+    if (!hw) return GOSSIP_OK;
+    const uint64_t words = ft_words(hw);
+    uint64_t* rv = reinterpret_cast<uint64_t*>(d_ftrecv);
+    int rc = ensure_dev(rv, ftrecv_cap, (words * R + 1) / 2);
+    d_ftrecv = reinterpret_cast<uint32_t*>(rv);
+    if (rc) return rc;
+    if ((rc = ft_pack(t))) return rc;
+    COMM_TRY(ncclAllGather(d_ftmsg, d_ftrecv, words, ncclUint32, comm, stream));
+    for (uint32_t r = 0; r < R; r++)
+        if (r != row_rank && (rc = ft_unpack(t, r, d_ftrecv + words * r))) return rc;
+    return GOSSIP_OK;
+}
+
 int gossip_engine::tick_step_b(int64_t t) {
     const int lv = (int)(t % 3);
     const uint32_t wact = hw;
     const int nxt = fcur ^ 1;
-    if (comm) {
+    if (comm && fused_rows) {
+        int rc = exchange_ft(t);
+        if (rc) return rc;
+    } else if (comm) {
         int rc = exchange_rccl(t);
         if (rc) return rc;
     } else if (opt_rehearse_rows > 1 && !young && hw) {
@@ -3473,6 +3560,7 @@ int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end
             return set_error(GOSSIP_EINVAL, "group run: every engine must be on the same device (no peer access)");
     }
     gossip_engine* e0 = es[0];
+    for (uint32_t r = 0; r < count; r++) es[r]->group_mode = true;
     if (tick_end > e0->tick_end) tick_end = e0->tick_end;
     try {
         while (e0->cur < tick_end) {
@@ -3497,8 +3585,26 @@ int gossip_engine_group_run(gossip_engine** es, uint32_t count, int64_t tick_end
             // the collectives (the ranks already ran one after another, so nothing overlaps here):
             // the same device-sized messages, capacities and second rounds as exchange_rccl
             for (uint32_t r = 1; r < count; r++)
-                if (es[r]->nchunks != e0->nchunks) return set_error(GOSSIP_EINVAL, "ranks use different xchunks options");
-            for (uint32_t c = 0; c < e0->nchunks; c++) {
+                if (es[r]->nchunks != e0->nchunks || es[r]->fused_rows != e0->fused_rows)
+                    return set_error(GOSSIP_EINVAL, "ranks use different xchunks / dense_fused options");
+            // the fused tick's FT slice exchange (exchange_ft): every rank packs, then every rank
+            // unpacks the others' messages in place (one device)
+            if (e0->fused_rows && e0->hw) {
+                for (uint32_t r = 0; r < count; r++) {
+                    int rc = es[r]->ft_pack(t);
+                    if (rc) return rc;
+                    HIP_TRY(hipStreamSynchronize(es[r]->stream));
+                }
+                for (uint32_t d = 0; d < count; d++) {
+                    for (uint32_t r = 0; r < count; r++) {
+                        if (r == d) continue;
+                        int rc = es[d]->ft_unpack(t, r, es[r]->d_ftmsg);
+                        if (rc) return rc;
+                    }
+                    HIP_TRY(hipStreamSynchronize(es[d]->stream));
+                }
+            }
+            for (uint32_t c = 0; c < e0->nchunks && !e0->fused_rows; c++) {
                 auto geom = [&](uint32_t r, uint64_t* lo, uint64_t* hi, uint32_t* wl) {
                     e0->chunk_rows(r, c, lo, hi);
                     *wl = (c + 1 >= e0->nchunks) ? e0->hw : 0u;

@@ -32,18 +32,22 @@ def _engine(gossip, n, t_cut, topo, ev, mode, flags, part=None, snaps=()):
     return e
 
 
+# dense ranks run the fused tick (k_dense_fused over their own rows, FT slices exchanged: round 6)
+# unless "dense3" (dense_fused 0: the three-kernel pull and the chunked F-row exchange)
 @pytest.mark.parametrize("mode,n,p,R,batch,xchunks", [
     ("csr", 1500, 0.01, 2, False, 4),
     ("csr", 1500, 0.01, 3, False, 1),
     ("dense", 1200, 0.3, 2, False, 4),
+    ("dense3", 1200, 0.3, 2, False, 4),
     ("csr", 1100, 0.02, 2, True, 2),
     ("dense", 1100, 0.3, 2, True, 1),
     ("csr", 5000, 0.004, 2, False, 3),   # chunks of 1,024 rows, none empty
-    ("dense", 2100, 0.3, 2, False, 16),  # many empty chunks
+    ("dense", 1500, 0.3, 3, False, 16),  # ranks of 512, 512, 476 rows: 1,024-node stage 0 spans two
+    ("dense3", 2100, 0.3, 2, False, 16),  # many empty chunks
 ])
 def test_group_run_matches_single_engine_and_oracle(gossip, oracle, mode, n, p, R, batch, xchunks):
     topo, t_cut, ev = _inputs(gossip, n, p, 31, 7.3)
-    m = gossip.MODE_DENSE if mode == "dense" else gossip.MODE_CSR
+    m = gossip.MODE_DENSE if mode.startswith("dense") else gossip.MODE_CSR
     flags = gossip.F_HOP_BATCH if batch else 0
     snaps = [gossip.seconds_to_ns(6.0), gossip.seconds_to_ns(7.0)]
     ref = _engine(gossip, n, t_cut, topo, ev, m, flags, snaps=snaps)
@@ -54,10 +58,18 @@ def test_group_run_matches_single_engine_and_oracle(gossip, oracle, mode, n, p, 
     ranks = [_engine(gossip, n, t_cut, topo, ev, m, flags, part=(r, R), snaps=snaps) for r in range(R)]
     for e in ranks:  # pipelined exchange: rows pulled and exchanged in xchunks row chunks
         e.set_option("xchunks", xchunks)
+        if mode == "dense3":
+            e.set_option("dense_fused", 0)
     gossip.group_run(ranks)
     for e in ranks:
         e.sync()
     got = [e.stats() for e in ranks]
+    for e in ranks:  # every dense tick of every rank fused (unique ids), or none
+        c = e.counters()
+        if mode == "dense":
+            assert c.dense_fused_launches == c.pull_launches > 0 and c.exchange_bytes_sent > 0
+        elif mode == "dense3":
+            assert c.dense_fused_launches == 0
     for k in SUM:
         total = sum(getattr(g, k).astype(np.uint64) for g in got)
         assert np.array_equal(total, getattr(want, k).astype(np.uint64)), k

@@ -408,11 +408,17 @@ def test_c5_row_partition_sums_to_single(gossip, c5, ranks):
         engs.append(e)
     gossip.group_run(engs)
     parts = [e.stats() for e in engs]
+    cs = [e.counters() for e in engs]
     for e in engs:
         e.close()
     tot = _sum(parts)
     for k in SUM_STATS:
         assert np.array_equal(tot[k], getattr(whole, k).astype(np.uint64)), (ranks, k)
+    # every rank's every tick ran k_dense_fused over its own rows (round 6) and the ranks exchanged
+    # FT slices: per tick, each rank sends its rows' bits of every window column
+    for c in cs:
+        assert c.dense_fused_launches == c.pull_launches > 0, (c.dense_fused_launches, c.pull_launches)
+        assert c.exchange_bytes_sent >= c.pull_launches * 4096 * (topo.num_nodes // ranks) // 8
 
 
 # ------------------------------------------------------------------------------------------- C2

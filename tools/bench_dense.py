@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--row-shards", type=int, default=0,
                     help="rehearse an R-rank row partition on this GPU (gossip.group_run): reports "
                          "the per-rank MFMA kernel time and the frontier exchange volume per tick")
+    ap.add_argument("--three-kernels", action="store_true", help="A/B: dense_fused 0 (row exchange of F rows)")
     a = ap.parse_args()
     if a.config == "c2":
         n = a.nodes or 4096
@@ -76,6 +77,8 @@ def main():
         engs = []
         for r in range(R):
             e = gossip.Engine(topo.num_nodes, L, T0, t_cut, mode=gossip.MODE_DENSE, flags=gossip.F_TIMING)
+            if a.three_kernels:
+                e.set_option("dense_fused", 0)
             e.set_row_partition(r, R)
             e.set_topology(topo)
             e.set_schedule(ev)
@@ -90,19 +93,34 @@ def main():
         ops = [c.dense_ops for c in cs]
         ms = [c.pull_ms / max(c.pull_launches, 1) for c in cs]
         util = [o / (c.pull_ms * 1e-3) / INT8_PEAK_OPS if c.pull_ms else None for o, c in zip(ops, cs)]
+        # the DENSE phase by the device stamps (engine.hip k_phase_start / k_phase_acc: on a fused
+        # tick the kernel's own block-0 start to last-block end): contraction + dedup + FT_next
+        pms = [c.pull_phase_ms / max(c.pull_launches, 1) for c in cs]
+        putil = [o / (c.pull_phase_ms * 1e-3) / INT8_PEAK_OPS if c.pull_phase_ms else None for o, c in zip(ops, cs)]
         edge = sum(c.edge_events for c in cs)
-        n_ = topo.num_nodes
+        fused = all(c.dense_fused_launches == c.pull_launches for c in cs)
+        xb = [c.exchange_bytes_sent / max(c.pull_launches, 1) for c in cs]
+        xr = [c.exchange_bytes_received / max(c.pull_launches, 1) for c in cs]
+        # xGMI: a rank receives the other R - 1 messages over its 7 links (MI355X_MICROARCH.md:
+        # ~153 GB/s each); an estimate, not a measurement -- this box has one GPU
+        x_ms = max(xr) / (7 * 153e9) * 1e3
         out = {"workload": desc, "mode": f"dense, row partition x{R} rehearsed on 1 GPU (group_run)",
                "ticks": cs[0].ticks, "edge_events": edge,
+               "every_tick_fused_on_every_rank": fused,
+               "per_rank_fused_launches": [c.dense_fused_launches for c in cs],
+               "per_rank_phase_ms_avg": pms, "per_rank_phase_util": putil,
+               "per_rank_phase_ms_max": max(pms), "per_rank_phase_util_min": min(u for u in putil if u),
                "per_rank_mfma_ms_avg": ms, "per_rank_mfma_util": util,
-               "per_rank_mfma_ms_max": max(ms),
-               # NOT a throughput: an upper bound from the slowest rank's MFMA kernel alone
-               "mfma_kernel_only_bound_excl_exchange_and_dedup": edge / (cs[0].ticks * max(ms) * 1e-3),
-               "exchange_bytes_per_tick_per_rank": (n_ - n_ // R) * cs[0].words_hw * 8,
+               "exchange_bytes_sent_per_tick_per_rank": xb, "exchange_bytes_received_per_tick_per_rank": xr,
+               "exchange": "FT slices (each rank's nodes' bits of every window column, the stage masks "
+                           "and its partial liveness), one all-gather per tick",
+               "xgmi_ms_per_tick_estimate_unmeasured": x_ms,
+               "projected_tick_ms_unmeasured": max(pms) + x_ms,
+               "projected_edge_events_per_s_unmeasured": edge / (cs[0].ticks * (max(pms) + x_ms) * 1e-3),
                "group_wall_s_serialised": wall,
-               "note": "the bound uses only the per-tick time of the slowest rank's MFMA kernel: the "
-                       "exchange (all-gather of the frontier rows) and the dedup are not in it, so it "
-                       "is not an edge-event rate and must not be quoted as one"}
+               "note": "per-rank phase times are measured (ranks run one after another on one GPU); "
+                       "the 8-GPU tick adds the all-gather, estimated from the bytes at 7 x 153 GB/s "
+                       "of xGMI per rank, unmeasured on an 8-GPU node (no exchange overlap assumed)"}
         print(json.dumps(out), flush=True)
         return
     ref = None
