@@ -615,6 +615,13 @@ def main():
                 "traffic": traffic,
                 "kernel": "pull phase: k_pull + k_pull_young" +
                           (" (concurrent, two streams)" if overlap else " (in sequence)"),
+                # what `frac` is a fraction of: the bytes the skipping pull must move,
+                # itemised per kernel below; SURVEY 8(d)'s dense formula, which assumes every peer-row
+                # word is read, gives the second ratio (> 1: the kernels skip most of those rows)
+                "frac_basis": "achieved = algorithmic bytes of the skipping pull (k_pull's peer rows, "
+                              "ids, occupancy, own rows, counters + k_pull_young's slot lines, lists, rows) "
+                              "/ phase time; peak = 8 TB/s",
+                "dense_formula_frac": ((dense_bytes_per_launch / (ph_ms * 1e6)) / HBM_PEAK_GBS) if ph_ms > 0 else None,
                 "avg_launch_ms": ph_ms,
                 "launches": launches,
                 "bytes_per_launch": ph_b,

@@ -364,8 +364,10 @@ PUSH = {"forced": {"pull_push": 1}, "forced_young": {"pull_push": 1, "young": 1}
         "auto": {"pull_push": -1}, "off": {"pull_push": 0}}
 
 
-@pytest.mark.parametrize("case", ["wide_collisions", "odd_latency_cut", "packed_tiles"])
-@pytest.mark.parametrize("opts", list(PUSH))
+@pytest.mark.parametrize("case,opts", [(c, o) for c in ("wide_collisions", "odd_latency_cut", "packed_tiles")
+                                        for o in ("forced", "forced_young", "auto")] +
+                         [("packed_tiles", "forced_dense_rows"), ("wide_collisions", "forced_nt"),
+                          ("packed_tiles", "off")])
 def test_push_marks(gossip, oracle, case, opts):
     n, deg, seed, sim, lat_ms, id_mask, fl = {
         "wide_collisions": (3000, 8.0, 45, 6.3, 5.0, 0xFFF, gossip.F_TILE_PER_TICK),
