@@ -108,3 +108,13 @@ def test_fused_hop_batched_snapshots(gossip, oracle):
     for k in STATS:
         assert np.array_equal(getattr(fs, k), getattr(r, k)), k
     assert fc.words_hw >= 64  # > 16 column tiles in flight
+
+
+@pytest.mark.parametrize("n,p,seed", [(3000, 0.1, 78), (2048, 0.3, 79)])
+def test_fused_every_tile_split(gossip, oracle, monkeypatch, n, p, seed):
+    # GOSSIP_DENSE_ROUNDS=0: no whole-tile rounds, every live tile goes through the load-balanced
+    # tail, so most tiles are split between blocks and meet in the inc / ticket reduction
+    # (dense_kernel.h split-tile path: each wave's atomics acknowledged before the ticket)
+    monkeypatch.setenv("GOSSIP_DENSE_ROUNDS", "0")
+    flags = gossip.F_HOP_BATCH if n == 2048 else 0
+    _check(gossip, oracle, n, p, seed, 5.6 if not flags else 12.0, 5.0, flags=flags, expect_all_fused=True)
