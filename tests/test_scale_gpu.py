@@ -329,7 +329,7 @@ def test_c4_bench_slice_equals_continuous_run(gossip, c4):
     assert np.array_equal(a1.gen, np.bincount(gens["node"], minlength=n).astype(np.uint32))
     # later generations of ids whose earlier flood already covered the node: counted, not processed
     assert int((a1.gen.astype(np.int64) + a1.recv - a1.processed).sum()) > 0
-    assert ca1.words_hw > 200 and int(a1.recv.sum()) > 100 * len(gens)
+    assert ca1.words_hw > 100 and int(a1.recv.sum()) > 100 * len(gens)  # (a sixteenth: ~160 words)
     # the bench's pull: young-tile slots, the early exit on every tile
     assert ca1.young_launches > 0 and ca1.pull_late_age == 1
 
